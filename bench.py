@@ -1,0 +1,245 @@
+"""bench.py -- SGC propagation hot path on MI355X: propagated edges/s.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--shape reddit]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Metric (BASELINE.json): propagated edges/s = hops * nnz(S) / t, where t is
+one sgc_precompute (all K hops of S.X, reference utils.py:92-97) over the
+synthetic Reddit-shape graph (232,965 nodes, 11,606,919 undirected edges,
+nnz(S) = 23,446,803, F = 602, K = 2), inputs resident in HBM.
+A "step" = one full K-hop propagation.  N > 1: S row-partitioned over ranks
+(nnz-balanced), one RCCL all-gather of X per hop (sgc_amd.distributed);
+total work is fixed, so scaling is "strong".
+
+Also printed (same JSON line):
+  roofline      dominant kernel (the CSR SpMM) -- algorithmic bytes per hop
+                (gather model: 4(N+1) + 8nnz + 4F nnz + 4F N) / the kernel's
+                mean duration measured with events on the launch stream;
+                `traffic` = HBM bytes per launch from rocprofv3 PMC counters
+                when profiles/pmc_<shape>.json exists (else null)
+  cpu_baseline  the reference's arithmetic as written -- torch.spmm(COO, X)
+                (utils.py:95) on this host's CPU, one hop, rank 0 at N = 1
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from sgc_amd import graphs  # noqa: E402
+from sgc_amd.propagate import DeviceCSR, spmm  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes_per_hop(n, nnz, F):
+    return 4 * (n + 1) + 8 * nnz + 4 * F * nnz + 4 * F * n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def cpu_baseline(S, X_host, budget_s=30.0):
+    """The reference's arithmetic on this host: torch.spmm(COO, X) -- what
+    utils.py:95 runs each hop.  One hop over the full graph after a warm-up
+    hop on 64 feature columns (allocator first touch).  aten's COO kernel is
+    single-threaded whatever torch.get_num_threads() says, so
+    cores = 1.  Also times the CSR variant at all threads (bit-identical
+    output, the best CPU torch path) when the budget allows."""
+    rows, cols, vals = S.coo()
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([rows, cols])),
+                                  torch.from_numpy(vals), (S.n, S.n))
+    X = torch.from_numpy(X_host)
+    torch.spmm(adj, X[:, :64].contiguous())
+    t0 = time.perf_counter()
+    torch.spmm(adj, X)
+    t_coo = time.perf_counter() - t0
+    rec = {"value": S.nnz / t_coo, "unit": "edges/s", "cores": 1, "kind": "reference",
+           "sample": f"1 hop of torch.spmm(COO fp32 {S.n}x{S.n}, nnz {S.nnz}; X [{S.n},{X.shape[1]}]) "
+                     f"on the host CPU = reference utils.py:95 as written, after a 64-column "
+                     f"warm-up; {t_coo:.2f} s",
+           "host_cpu": cpu_model(), "os_cpu_count": os.cpu_count(),
+           "torch_threads": torch.get_num_threads()}
+    if t_coo < budget_s / 3:
+        csr = adj.to_sparse_csr()
+        torch.sparse.mm(csr, X)
+        t0 = time.perf_counter()
+        torch.sparse.mm(csr, X)
+        t_csr = time.perf_counter() - t0
+        rec["csr_all_threads"] = {"value": S.nnz / t_csr, "unit": "edges/s",
+                                  "cores": torch.get_num_threads(), "seconds": round(t_csr, 3)}
+    return rec
+
+
+def load_traffic(shape):
+    p = os.path.join(ROOT, "profiles", f"pmc_{shape}.json")
+    if not os.path.exists(p):
+        return None, None
+    with open(p) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--shape", default="reddit", choices=sorted(graphs.SHAPES))
+    ap.add_argument("--hops", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--threshold", type=int, default=None, help="heavy-row threshold")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    spec = graphs.SHAPES[args.shape]
+    K = args.hops or spec["hops"]
+    t_gen = time.perf_counter()
+    S = graphs.synthetic_graph(args.shape, seed=args.seed)
+    X_host = graphs.synthetic_features(args.shape, S.n, spec["features"], seed=args.seed + 1)
+    t_gen = time.perf_counter() - t_gen
+    n, F, nnz = S.n, X_host.shape[1], S.nnz
+    X0 = torch.from_numpy(X_host).to(dev)
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps * K)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps * K)]
+    ev = {"i": 0, "on": False}
+
+    if world == 1:
+        csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
+        csr.plan(0, n, args.threshold)
+        bufs = [torch.empty((n, F), device=dev), torch.empty((n, F), device=dev)]
+
+        def step():
+            src = X0
+            for h in range(K):
+                dst = bufs[(K - 1 - h) & 1]
+                if ev["on"]:
+                    starts[ev["i"]].record()
+                spmm(csr, src, out=dst, threshold=args.threshold)
+                if ev["on"]:
+                    ends[ev["i"]].record()
+                    ev["i"] += 1
+                src = dst
+            return src
+        parallelism = "single-gpu"
+    else:
+        from sgc_amd.distributed import RowPartitionedPropagator, make_shard
+        shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
+        from sgc_amd.distributed import _default_spmm
+
+        def timed_spmm(sh, col, X, out):
+            if ev["on"]:
+                starts[ev["i"]].record()
+            r = _default_spmm(sh, col, X, out)
+            if ev["on"]:
+                ends[ev["i"]].record()
+                ev["i"] += 1
+            return r
+        prop = RowPartitionedPropagator(shard, spmm_fn=timed_spmm)
+        out_full = torch.empty((n, F), device=dev)
+
+        def step():
+            return prop.propagate(X0, K, out=out_full)
+        parallelism = f"row-partition x{world} + rccl all-gather per hop"
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev["on"] = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ev["on"] = False
+    kern_ms = [s.elapsed_time(e) for s, e in zip(starts[:ev["i"]], ends[:ev["i"]])]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = K * nnz * args.steps / elapsed
+    kern_mean_ms = float(np.mean(kern_ms)) if kern_ms else float("nan")
+    if world == 1:
+        bytes_launch = algorithmic_bytes_per_hop(n, nnz, F)
+        unit_desc = f"one hop over all {n} rows"
+    else:
+        rows = shard.rows
+        nnz_l = int(shard.row_ptr[-1].item())
+        bytes_launch = 4 * (rows + 1) + 8 * nnz_l + 4 * F * nnz_l + 4 * F * rows
+        unit_desc = f"one hop over rank 0's {rows} rows ({nnz_l} nnz)"
+    achieved = bytes_launch / (kern_mean_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(args.shape) if world == 1 else (None, None)
+
+    rec = None
+    if rank == 0:
+        rec = {
+            "metric": "propagated edges/sec (K-hop SpMM), Reddit-shape K=2",
+            "value": value,
+            "unit": "edges/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded R-MAT graph + AugNorm, SURVEY.md 8(d))",
+            "config": {"workload": f"{args.shape}-shape sgc_precompute K={K}", "nodes": n,
+                       "undirected_edges": spec["edges"], "nnz": nnz, "features": F, "hops": K,
+                       "parallelism": parallelism, "heavy_threshold": args.threshold},
+            "precompute_seconds": ms_per_step / 1e3,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "spmm_csr_kernel", "kernel_mean_ms": kern_mean_ms,
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "launch_unit": unit_desc, "traffic_source": traffic_src,
+                         "compulsory_bytes_per_hop": 4 * (n + 1) + 8 * nnz + 8 * F * n},
+            "generate_seconds": round(t_gen, 2),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(S, X_host)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,126 @@
+/*
+ * sgc_amd.h -- C ABI of libsgc_amd.so, the MI355X (gfx950) propagation engine
+ * behind SGC's sgc_precompute() / SGC.forward().
+ *
+ * The reference (bellaj09/SGC) has no native code and no FFI: its hot path is
+ * three lines of Python calling torch (utils.py:92-97 -> torch.spmm at
+ * utils.py:95; models.py:17-18 -> nn.Linear).  Each entry point below names
+ * the reference call it replaces.  Conventions:
+ *
+ *   - every pointer is a DEVICE pointer unless the parameter name ends in
+ *     _host; buffers are owned by the caller (torch), never freed here;
+ *   - `stream` is a hipStream_t passed as void* (torch:
+ *     torch.cuda.current_stream().cuda_stream); all work is enqueued
+ *     asynchronously on it; nothing here synchronises the device except the
+ *     calls documented as "synchronous";
+ *   - return 0 on success, a positive SGC_E* code on failure;
+ *     sgc_last_error() returns a thread-local message for the last failure;
+ *   - indices are int32 (n_rows, n_cols, nnz < 2^31), values fp32.
+ */
+#ifndef SGC_AMD_H
+#define SGC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SGC_ABI_VERSION 1
+
+enum {
+    SGC_OK = 0,
+    SGC_EINVAL = 1,   /* bad argument (shape, stride, alignment, null)   */
+    SGC_ERANGE = 2,   /* size or index outside the int32 CSR limits      */
+    SGC_EHIP = 3,     /* a HIP runtime call failed                       */
+    SGC_ENOMEM = 4,   /* workspace too small                             */
+    SGC_EDEVICE = 5   /* no gfx950 device / kernel image not loadable    */
+};
+
+int sgc_abi_version(void);
+const char *sgc_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Ingest: torch sparse COO -> CSR.
+ * Replaces the implicit COO handling inside torch.spmm (utils.py:95) for the
+ * adjacency built by sparse_mx_to_torch_sparse_tensor (utils.py:23-30:
+ * int64 [2,nnz] indices, fp32 values).  The CSR keeps every stored entry
+ * (no coalescing) and, within a row, the COO storage order (stable by row),
+ * which is the order torch's CPU kernel applies its FMAs in.
+ *
+ * sgc_coo_to_csr_workspace: bytes of device scratch sgc_coo_to_csr needs.
+ * sgc_coo_to_csr: rows/cols are the two rows of the [2,nnz] index tensor.
+ *   status_host (synchronous; may be NULL to stay asynchronous) receives a
+ *   bit set: 1 = input rows already sorted, 2 = every CSR row has strictly
+ *   ascending columns, 4 = an index was out of range (CSR then invalid).
+ * ------------------------------------------------------------------------- */
+int sgc_coo_to_csr_workspace(int64_t n_rows, int64_t nnz, size_t *bytes_host);
+int sgc_coo_to_csr(const int64_t *rows, const int64_t *cols, const float *vals,
+                   int64_t nnz, int64_t n_rows, int64_t n_cols,
+                   int32_t *row_ptr, int32_t *col_idx, float *val_out,
+                   void *workspace, size_t workspace_bytes,
+                   uint32_t *status_host, void *stream);
+
+/* Same, from torch CSR (crow_indices/col_indices int64): narrows to int32. */
+int sgc_csr64_to_csr(const int64_t *crow, const int64_t *col, const float *vals,
+                     int64_t nnz, int64_t n_rows, int64_t n_cols,
+                     int32_t *row_ptr, int32_t *col_idx, float *val_out,
+                     uint32_t *status_host, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Schedule ("plan") for the SpMM.  Lists the rows of [row_begin, row_end)
+ * with more than heavy_threshold nonzeros, heaviest first.  sgc_spmm_csr_f32
+ * runs each listed row as one work item per 64V-float feature chunk (so a
+ * power-law hub runs on several wavefronts at once, scheduled first) and
+ * every other row as one work item.  The plan changes only the schedule:
+ * every output element is still one sequential FMA chain, so results never
+ * depend on it.  Synchronous (reads the heavy-row list back to sort it).
+ *
+ * plan must hold sgc_plan_capacity(row_end - row_begin) int32 words;
+ * *n_heavy_host receives the number of heavy rows written to plan[0..).
+ * ------------------------------------------------------------------------- */
+int64_t sgc_plan_capacity(int64_t n_rows);
+int sgc_plan_build(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
+                   int32_t heavy_threshold, int32_t *plan, int64_t plan_capacity,
+                   int64_t *n_heavy_host, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * One hop Y = S[row_begin:row_end, :] . X  (utils.py:95, torch.spmm).
+ * Y row 0 receives S row row_begin.  Each Y[i,f] is
+ *     acc = +0.0f; for k in row i (CSR order): acc = fmaf(val[k], X[col[k], f], acc)
+ * -- bit-identical to the reference CPU kernel.  X rows have stride ldx
+ * floats, Y rows ldy floats; X must not alias Y.
+ * plan/n_heavy/heavy_threshold from sgc_plan_build over the same row range,
+ * or plan = NULL (one work item per row, natural order).
+ * ------------------------------------------------------------------------- */
+int sgc_spmm_csr_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                     int64_t row_begin, int64_t row_end,
+                     const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
+                     const int32_t *plan, int64_t n_heavy, int32_t heavy_threshold,
+                     void *stream);
+
+/* K hops X_K = S^K X_0 over all n_rows rows (utils.py:92-97, the whole
+ * sgc_precompute loop), ping-ponging between out and work so the last hop
+ * lands in out.  out has row stride ldo; work is n_rows*F floats (ld = F,
+ * may be NULL when K <= 1).  K = 0 copies X_0 into out (the Python layer
+ * returns the input object itself, as the reference does). */
+int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                      int64_t n_rows, const float *X0, int64_t ldx, float *out,
+                      int64_t ldo, float *work, int64_t F, int32_t K,
+                      const int32_t *plan, int64_t n_heavy, int32_t heavy_threshold,
+                      void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Classifier forward Y[M,C] = X[M,K] . W[C,K]^T + b[C]  (models.py:17-18,
+ * nn.Linear) on fp32 MFMA (v_mfma_f32_16x16x4_f32).  b may be NULL.
+ * X row stride ldx, Y row stride ldy.  Tolerance-equal to torch (summation
+ * order differs), not bit-equal.
+ * ------------------------------------------------------------------------- */
+int sgc_linear_f32(const float *X, int64_t ldx, const float *W, const float *b,
+                   float *Y, int64_t ldy, int64_t M, int64_t K, int64_t C, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGC_AMD_H */

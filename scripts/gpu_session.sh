@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace.
+# Every GPU step has its own time limit; a fault-like exit (anything but 0/1:
+# timeout 124/137, abort 134, segfault 139) stops the session.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+ROOTDIR=$(pwd)
+OUT=$ROOTDIR/gpurun_out
+mkdir -p "$OUT"
+STEPS=${STEPS:-"pytest smoke bench prof"}
+run() {
+  local name=$1; shift
+  local t0=$(date +%s)
+  "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc $(( $(date +%s) - t0 ))s"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fault-like exit from $name; stopping"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    pytest) run pytest timeout -k 10 900 python -m pytest tests -x -q -m gpu ;;
+    smoke)  run smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  run bench timeout -k 10 600 python bench.py ${BENCH_ARGS} ;;
+    prof)   cd /tmp && export TMPDIR=/tmp && \
+            run prof timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
+                --output-format csv -- python3 "$ROOTDIR/bench.py" --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS}
+            cd "$ROOTDIR" ;;
+  esac
+done

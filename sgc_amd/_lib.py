@@ -1,0 +1,78 @@
+"""ctypes binding of libsgc_amd.so (C ABI: include/sgc_amd.h).
+
+The product path always runs the HIP kernels: if the library is missing or
+cannot be loaded, every call raises -- there is no CPU or torch fallback.
+torch is imported first so the library's libamdhip64.so.7 dependency binds to
+the HIP runtime torch already loaded (one runtime per process).
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see above)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SGC_AMD_LIB", os.path.join(_HERE, "libsgc_amd.so"))
+
+_i64, _i32, _u32 = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32
+_p, _sz = ctypes.c_void_p, ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/sgc_amd.h one for one.
+SIGNATURES = {
+    "sgc_abi_version": (ctypes.c_int, []),
+    "sgc_last_error": (ctypes.c_char_p, []),
+    "sgc_coo_to_csr_workspace": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
+    "sgc_coo_to_csr": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _p, _sz,
+                                      ctypes.POINTER(_u32), _p]),
+    "sgc_csr64_to_csr": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _p, _p, _p,
+                                        ctypes.POINTER(_u32), _p]),
+    "sgc_plan_capacity": (_i64, [_i64]),
+    "sgc_plan_build": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, ctypes.POINTER(_i64), _p]),
+    "sgc_spmm_csr_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
+                                        _p, _i64, _i32, _p]),
+    "sgc_propagate_f32": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32,
+                                         _p, _i64, _i32, _p]),
+    "sgc_linear_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+}
+
+ABI_VERSION = 1
+_lib = None
+
+
+class SGCError(RuntimeError):
+    pass
+
+
+def load():
+    """Load and type the library (once).  Raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SGCError(
+            f"sgc_amd: native library {LIB_PATH} not found; build it with "
+            "`python -m sgc_amd.build` (hipcc --offload-arch=gfx950). "
+            "There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.sgc_abi_version() != ABI_VERSION:
+        raise SGCError(f"sgc_amd: ABI mismatch ({lib.sgc_abi_version()} != {ABI_VERSION})")
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().sgc_last_error().decode(errors="replace")
+        raise SGCError(f"sgc_amd: {what} failed (code {rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,51 @@
+// common.h -- shared helpers for the gfx950 kernels of libsgc_amd.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sgc_amd.h"
+
+namespace sgc {
+
+// Thread-local message for sgc_last_error().
+void set_error(const char *fmt, ...);
+
+#define SGC_HIP_CHECK(expr)                                                         \
+    do {                                                                            \
+        hipError_t _e = (expr);                                                     \
+        if (_e != hipSuccess) {                                                     \
+            ::sgc::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                             __FILE__, __LINE__);                                   \
+            return SGC_EHIP;                                                        \
+        }                                                                           \
+    } while (0)
+
+#define SGC_REQUIRE(cond, code, ...)       \
+    do {                                   \
+        if (!(cond)) {                     \
+            ::sgc::set_error(__VA_ARGS__); \
+            return (code);                 \
+        }                                  \
+    } while (0)
+
+static constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// V consecutive fp32 in one lane: float / float2 / float4 register vectors,
+// loaded with one global_load_dword{,x2,x4}.
+template <int V> struct Vec { typedef float __attribute__((ext_vector_type(V))) T; };
+template <> struct Vec<1> { typedef float T; };
+
+template <int V>
+__device__ __forceinline__ float lane_elem(const typename Vec<V>::T &x, int i) { return x[i]; }
+template <>
+__device__ __forceinline__ float lane_elem<1>(const float &x, int) { return x; }
+
+template <int V>
+__device__ __forceinline__ void set_elem(typename Vec<V>::T &x, int i, float v) { x[i] = v; }
+template <>
+__device__ __forceinline__ void set_elem<1>(float &x, int, float v) { x = v; }
+
+}  // namespace sgc

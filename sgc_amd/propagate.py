@@ -1,0 +1,238 @@
+"""Device CSR, SpMM and K-hop propagation on gfx950 through libsgc_amd.so.
+
+This is the engine under the drop-in `sgc_precompute` (reference
+utils.py:92-97).  Host code only marshals torch tensors into the C ABI
+(include/sgc_amd.h); every byte of arithmetic runs in the HIP kernels.
+"""
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+# Rows with more nonzeros than this are split into per-feature-chunk work
+# items and scheduled first (see sgc_plan_build).  Results never depend on it.
+DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SGC_AMD_HEAVY_THRESHOLD", "512"))
+
+STATUS_ROWS_SORTED = 1
+STATUS_COLS_ASCENDING = 2
+STATUS_OUT_OF_RANGE = 4
+
+
+def _require_device(t, what):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"sgc_amd: {what} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"sgc_amd: {what} is on {t.device}; the propagation engine runs only on a "
+            "ROCm (gfx950) device -- move tensors with .cuda() (no CPU fallback)")
+
+
+@dataclass
+class DeviceCSR:
+    """int32 CSR of the normalised adjacency S, resident in HBM.
+
+    Built once per adjacency tensor (cached on it) by a stable sort of the
+    COO entries by row: every stored entry is kept and each row keeps its
+    storage order, which is the FMA order of torch.spmm's CPU kernel."""
+    n_rows: int
+    n_cols: int
+    row_ptr: torch.Tensor  # int32 [n_rows+1]
+    col_idx: torch.Tensor  # int32 [nnz]
+    val: torch.Tensor      # float32 [nnz]
+    status: int = 0
+    ingest_seconds: float = 0.0
+    _plans: dict = field(default_factory=dict)
+
+    @property
+    def nnz(self):
+        return self.col_idx.numel()
+
+    @property
+    def device(self):
+        return self.row_ptr.device
+
+    @classmethod
+    def from_host_arrays(cls, row_ptr, col_idx, val, n_cols=None, device="cuda"):
+        """From host CSR arrays already in the SpMM's order (numpy or torch)."""
+        rp = torch.as_tensor(row_ptr).to(device=device, dtype=torch.int32)
+        ci = torch.as_tensor(col_idx).to(device=device, dtype=torch.int32)
+        va = torch.as_tensor(val).to(device=device, dtype=torch.float32)
+        n = rp.numel() - 1
+        return cls(n, n if n_cols is None else n_cols, rp.contiguous(), ci.contiguous(),
+                   va.contiguous())
+
+    @classmethod
+    def from_torch(cls, adj):
+        """From a torch sparse COO (reference utils.py:23-30 layout) or CSR tensor."""
+        import time
+        _require_device(adj, "adj")
+        if adj.dtype != torch.float32:
+            raise TypeError(f"sgc_amd: adj must be float32, got {adj.dtype}")
+        if adj.dim() != 2:
+            raise ValueError("sgc_amd: adj must be 2-D")
+        lib = _lib.load()
+        n_rows, n_cols = adj.shape
+        dev = adj.device
+        t0 = time.perf_counter()
+        with torch.cuda.device(dev):
+            stream = _lib.stream_handle(dev)
+            status = _lib._u32(0)
+            if adj.layout == torch.sparse_coo:
+                idx = adj._indices().contiguous()
+                vals = adj._values().contiguous()
+                nnz = vals.numel()
+                rows, cols = idx[0], idx[1]
+                row_ptr = torch.empty(n_rows + 1, dtype=torch.int32, device=dev)
+                col_idx = torch.empty(nnz, dtype=torch.int32, device=dev)
+                val = torch.empty(nnz, dtype=torch.float32, device=dev)
+                ws_bytes = _lib._sz(0)
+                _lib.check(lib.sgc_coo_to_csr_workspace(n_rows, nnz, ctypes_byref(ws_bytes)),
+                           "coo_to_csr_workspace")
+                ws = torch.empty(max(1, ws_bytes.value), dtype=torch.uint8, device=dev)
+                _lib.check(lib.sgc_coo_to_csr(_lib.ptr(rows), _lib.ptr(cols), _lib.ptr(vals), nnz,
+                                              n_rows, n_cols, _lib.ptr(row_ptr), _lib.ptr(col_idx),
+                                              _lib.ptr(val), _lib.ptr(ws), ws_bytes.value,
+                                              ctypes_byref(status), stream), "coo_to_csr")
+                del ws
+            elif adj.layout == torch.sparse_csr:
+                crow = adj.crow_indices().to(torch.int64).contiguous()
+                ccol = adj.col_indices().to(torch.int64).contiguous()
+                vals = adj.values().contiguous()
+                nnz = vals.numel()
+                row_ptr = torch.empty(n_rows + 1, dtype=torch.int32, device=dev)
+                col_idx = torch.empty(nnz, dtype=torch.int32, device=dev)
+                val = torch.empty(nnz, dtype=torch.float32, device=dev)
+                _lib.check(lib.sgc_csr64_to_csr(_lib.ptr(crow), _lib.ptr(ccol), _lib.ptr(vals),
+                                                nnz, n_rows, n_cols, _lib.ptr(row_ptr),
+                                                _lib.ptr(col_idx), _lib.ptr(val),
+                                                ctypes_byref(status), stream), "csr64_to_csr")
+            else:
+                raise TypeError(f"sgc_amd: unsupported adj layout {adj.layout}")
+        csr = cls(n_rows, n_cols, row_ptr, col_idx, val, int(status.value))
+        csr.ingest_seconds = time.perf_counter() - t0
+        return csr
+
+    def plan(self, row_begin=0, row_end=None, threshold=None):
+        """Heavy-row schedule for rows [row_begin, row_end) (cached)."""
+        row_end = self.n_rows if row_end is None else row_end
+        threshold = DEFAULT_HEAVY_THRESHOLD if threshold is None else int(threshold)
+        key = (row_begin, row_end, threshold)
+        if key not in self._plans:
+            lib = _lib.load()
+            n = row_end - row_begin
+            cap = lib.sgc_plan_capacity(n)
+            buf = torch.empty(max(1, cap), dtype=torch.int32, device=self.device)
+            n_heavy = _lib._i64(0)
+            with torch.cuda.device(self.device):
+                _lib.check(lib.sgc_plan_build(_lib.ptr(self.row_ptr), row_begin, row_end, threshold,
+                                              _lib.ptr(buf), cap, ctypes_byref(n_heavy),
+                                              _lib.stream_handle(self.device)), "plan_build")
+            h = int(n_heavy.value)
+            self._plans[key] = (buf[:max(h, 1)].clone(), h, threshold)
+        return self._plans[key]
+
+
+def ctypes_byref(x):
+    import ctypes
+    return ctypes.byref(x)
+
+
+def csr_of(adj):
+    """Cached DeviceCSR of a torch sparse adjacency (rebuilt if adj changed)."""
+    cached = getattr(adj, "_sgc_amd_csr", None)
+    if cached is not None and cached[0] == adj._version:
+        return cached[1]
+    csr = DeviceCSR.from_torch(adj)
+    try:
+        adj._sgc_amd_csr = (adj._version, csr)
+    except (AttributeError, RuntimeError):
+        pass
+    return csr
+
+
+def _check_features(X, csr):
+    _require_device(X, "features")
+    if X.device != csr.device:
+        raise RuntimeError(f"sgc_amd: features on {X.device} but adj on {csr.device}")
+    if X.dtype != torch.float32:
+        raise TypeError(f"sgc_amd: features must be float32, got {X.dtype}")
+    if X.dim() != 2 or X.shape[0] != csr.n_cols:
+        raise RuntimeError(f"sgc_amd: size mismatch, adj {csr.n_rows}x{csr.n_cols} . "
+                           f"features {tuple(X.shape)}")
+    if X.stride(1) != 1 or X.stride(0) < X.shape[1]:
+        X = X.contiguous()
+    return X
+
+
+def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
+         use_plan=True, threshold=None):
+    """One hop Y = S[row_begin:row_end] . X (bit-exact with torch.spmm on CPU)."""
+    X = _check_features(X, csr)
+    row_end = csr.n_rows if row_end is None else row_end
+    F = X.shape[1]
+    if out is None:
+        out = torch.empty((row_end - row_begin, F), dtype=torch.float32, device=X.device)
+    if F == 0 or row_end == row_begin:
+        return out
+    plan, n_heavy, thr = csr.plan(row_begin, row_end, threshold) if use_plan else (None, 0, 0)
+    lib = _lib.load()
+    with torch.cuda.device(X.device):
+        _lib.check(lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
+                                        _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
+                                        X.stride(0), _lib.ptr(out), out.stride(0), F,
+                                        _lib.ptr(plan), n_heavy, thr,
+                                        _lib.stream_handle(X.device)), "spmm_csr_f32")
+    return out
+
+
+def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, work=None, use_plan=True,
+              threshold=None):
+    """X_K = S^K X on the device (K >= 1); asynchronous on the current stream."""
+    X = _check_features(X, csr)
+    if csr.n_rows != csr.n_cols:
+        raise RuntimeError("sgc_amd: propagation needs a square adjacency")
+    n, F = X.shape
+    if out is None:
+        out = torch.empty((n, F), dtype=torch.float32, device=X.device)
+    if K > 1 and work is None:
+        work = torch.empty((n, F), dtype=torch.float32, device=X.device)
+    if n == 0 or F == 0:
+        return out
+    plan, n_heavy, thr = csr.plan(0, n, threshold) if use_plan else (None, 0, 0)
+    lib = _lib.load()
+    with torch.cuda.device(X.device):
+        _lib.check(lib.sgc_propagate_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
+                                         _lib.ptr(csr.val), n, _lib.ptr(X), X.stride(0),
+                                         _lib.ptr(out), out.stride(0),
+                                         _lib.ptr(work) if K > 1 else None, F, int(K),
+                                         _lib.ptr(plan), n_heavy, thr,
+                                         _lib.stream_handle(X.device)), "propagate_f32")
+    return out
+
+
+def linear(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, out=None):
+    """Y = X . W^T + b on fp32 MFMA (reference models.py:17-18, nn.Linear)."""
+    _require_device(X, "input")
+    if X.dtype != torch.float32 or weight.dtype != torch.float32:
+        raise TypeError("sgc_amd.linear: float32 only")
+    if X.dim() != 2:
+        raise ValueError("sgc_amd.linear: 2-D input expected")
+    M, K = X.shape
+    C = weight.shape[0]
+    if weight.shape[1] != K:
+        raise RuntimeError(f"sgc_amd.linear: shape mismatch {tuple(X.shape)} x {tuple(weight.shape)}^T")
+    if X.stride(1) != 1 or X.stride(0) < K:
+        X = X.contiguous()
+    W = weight.contiguous()
+    b = bias.contiguous() if bias is not None else None
+    if out is None:
+        out = torch.empty((M, C), dtype=torch.float32, device=X.device)
+    lib = _lib.load()
+    with torch.cuda.device(X.device):
+        _lib.check(lib.sgc_linear_f32(_lib.ptr(X), X.stride(0), _lib.ptr(W), _lib.ptr(b),
+                                      _lib.ptr(out), out.stride(0), M, K, C,
+                                      _lib.stream_handle(X.device)), "linear_f32")
+    return out
