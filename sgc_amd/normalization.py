@@ -47,5 +47,6 @@ def fetch_normalization(type):  # noqa: A002  (reference argument name)
 
 
 def row_normalize(mx):
-    r_inv = _inv_power(np.asarray(mx.sum(1), dtype=np.float64).ravel(), -1.0)
+    # keep the row sums' dtype (float32 features stay float32, as the reference's)
+    r_inv = _inv_power(np.asarray(mx.sum(1)).ravel(), -1)
     return sp.diags(r_inv).dot(mx)
