@@ -35,7 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from sgc_amd import graphs  # noqa: E402
-from sgc_amd.propagate import DeviceCSR, spmm  # noqa: E402
+from sgc_amd.propagate import DeviceCSR, propagate  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -106,6 +106,10 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threshold", type=int, default=None, help="heavy-row threshold")
+    ap.add_argument("--group-floats", type=int, default=128,
+                    help="N>1: feature-group width of the compute/all-gather pipeline")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo = host-staged rehearsal of the N>1 path (ranks may share a GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -114,10 +118,14 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    local_dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        else:
+            dist.init_process_group("gloo")
 
     spec = graphs.SHAPES[args.shape]
     K = args.hops or spec["hops"]
@@ -128,32 +136,35 @@ def main():
     n, F, nnz = S.n, X_host.shape[1], S.nnz
     X0 = torch.from_numpy(X_host).to(dev)
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps * K)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps * K)]
+    n_launch = args.steps * K * (1 if world == 1 else -(-F // max(2, args.group_floats)))
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(n_launch)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(n_launch)]
+    launch_bytes = []
     ev = {"i": 0, "on": False}
 
     if world == 1:
         csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
         csr.plan(0, n, args.threshold)
-        bufs = [torch.empty((n, F), device=dev), torch.empty((n, F), device=dev)]
+        out_buf = torch.empty((n, F), device=dev)
 
-        def step():
-            src = X0
-            for h in range(K):
-                dst = bufs[(K - 1 - h) & 1]
-                if ev["on"]:
-                    starts[ev["i"]].record()
-                spmm(csr, src, out=dst, threshold=args.threshold)
-                if ev["on"]:
-                    ends[ev["i"]].record()
-                    ev["i"] += 1
-                src = dst
-            return src
+        def hook(phase, h):
+            if not ev["on"]:
+                return
+            if phase == "start":
+                starts[ev["i"]].record()
+            else:
+                ends[ev["i"]].record()
+                ev["i"] += 1
+
+        def step():  # the product path of sgc_precompute (sgc_amd.propagate)
+            return propagate(csr, X0, K, out=out_buf, threshold=args.threshold, hop_hook=hook)
         parallelism = "single-gpu"
     else:
         from sgc_amd.distributed import RowPartitionedPropagator, make_shard
         shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
         from sgc_amd.distributed import _default_spmm
+
+        nnz_l = int(shard.row_ptr[-1].item())
 
         def timed_spmm(sh, col, X, out):
             if ev["on"]:
@@ -162,13 +173,18 @@ def main():
             if ev["on"]:
                 ends[ev["i"]].record()
                 ev["i"] += 1
+                fg = X.shape[1]
+                launch_bytes.append(4 * (sh.rows + 1) + 8 * nnz_l + 4 * fg * nnz_l + 4 * fg * sh.rows)
             return r
-        prop = RowPartitionedPropagator(shard, spmm_fn=timed_spmm)
+        prop = RowPartitionedPropagator(shard, spmm_fn=timed_spmm, group_floats=args.group_floats,
+                                        host_staging=args.dist_backend == "gloo")
         out_full = torch.empty((n, F), device=dev)
 
         def step():
             return prop.propagate(X0, K, out=out_full)
-        parallelism = f"row-partition x{world} + rccl all-gather per hop"
+        parallelism = (f"row-partition x{world} (nnz-balanced) + per-hop all-gather "
+                       f"({'rccl' if args.dist_backend == 'nccl' else 'gloo rehearsal'}), "
+                       f"pipelined in {args.group_floats}-float feature groups")
 
     for _ in range(args.warmup):
         step()
@@ -199,10 +215,9 @@ def main():
         bytes_launch = algorithmic_bytes_per_hop(n, nnz, F)
         unit_desc = f"one hop over all {n} rows"
     else:
-        rows = shard.rows
-        nnz_l = int(shard.row_ptr[-1].item())
-        bytes_launch = 4 * (rows + 1) + 8 * nnz_l + 4 * F * nnz_l + 4 * F * rows
-        unit_desc = f"one hop over rank 0's {rows} rows ({nnz_l} nnz)"
+        bytes_launch = float(np.mean(launch_bytes)) if launch_bytes else float("nan")
+        unit_desc = (f"one hop of one {args.group_floats}-float feature group over rank 0's "
+                     f"{shard.rows} rows ({nnz_l} nnz)")
     achieved = bytes_launch / (kern_mean_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(args.shape) if world == 1 else (None, None)
 

@@ -41,6 +41,14 @@ enum {
 int sgc_abi_version(void);
 const char *sgc_last_error(void);
 
+/* Process-wide schedule knobs (results never depend on them).
+ *   "slice_floats": feature-slice width of the SpMM grid (default 128;
+ *                   0 = one slice as wide as the registers allow);
+ *   "max_vec":      widest per-lane load, 1, 2 or 4 floats (default 4).
+ * sgc_get_tuning returns -1 for an unknown key. */
+int sgc_set_tuning(const char *key, int64_t value);
+int64_t sgc_get_tuning(const char *key);
+
 /* ---------------------------------------------------------------------------
  * Ingest: torch sparse COO -> CSR.
  * Replaces the implicit COO handling inside torch.spmm (utils.py:95) for the
@@ -101,15 +109,27 @@ int sgc_spmm_csr_f32(const int32_t *row_ptr, const int32_t *col_idx, const float
                      void *stream);
 
 /* K hops X_K = S^K X_0 over all n_rows rows (utils.py:92-97, the whole
- * sgc_precompute loop), ping-ponging between out and work so the last hop
- * lands in out.  out has row stride ldo; work is n_rows*F floats (ld = F,
- * may be NULL when K <= 1).  K = 0 copies X_0 into out (the Python layer
- * returns the input object itself, as the reference does). */
+ * sgc_precompute loop).  out (row stride ldo) receives X_K.  Intermediate
+ * hops live in the workspace with 128-B aligned rows (ld = F rounded up to 32
+ * floats: a gathered X row segment then spans the fewest 128-B lines); when
+ * X_0's rows are not 128-B aligned it is first copied into that layout
+ * (sgc_pad_rows_f32), which costs one streaming copy and saves ~9% per hop
+ * that reads it at Reddit shape.  K = 0 copies X_0 into out (the Python
+ * layer returns the input object itself, as the reference does).
+ * sgc_propagate_workspace: bytes of device workspace for these arguments. */
+int64_t sgc_propagate_workspace(int64_t n_rows, int64_t F, int64_t ldx, int32_t K);
 int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                       int64_t n_rows, const float *X0, int64_t ldx, float *out,
-                      int64_t ldo, float *work, int64_t F, int32_t K,
+                      int64_t ldo, int64_t F, int32_t K,
                       const int32_t *plan, int64_t n_heavy, int32_t heavy_threshold,
-                      void *stream);
+                      void *workspace, int64_t workspace_bytes, void *stream);
+
+/* Row-strided copy dst[i, 0:F] = src[i, 0:F] (re-layout of feature rows). */
+int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd,
+                     int64_t n_rows, int64_t F, void *stream);
+
+/* The row stride (floats) the engine uses for its own feature buffers. */
+int64_t sgc_aligned_ld(int64_t F);
 
 /* ---------------------------------------------------------------------------
  * Classifier forward Y[M,C] = X[M,K] . W[C,K]^T + b[C]  (models.py:17-18,

@@ -1,0 +1,99 @@
+"""Interleaved A/B timing of SpMM build variants and schedule thresholds in ONE
+process (cdna_hip_programming.md 5.4 rule 24), Reddit-shape hop.
+
+    python scripts/sweep.py [--libs a.so,b.so] [--thresholds 256,512,2048] [--rounds 8]
+
+Every variant must stay bit-identical: the first output of each is compared
+with the product library's.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from sgc_amd import _lib, graphs  # noqa: E402
+from sgc_amd.propagate import DeviceCSR  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", default="")
+    ap.add_argument("--thresholds", default="512")
+    ap.add_argument("--slices", default="128", help="slice_floats values (sgc_set_tuning)")
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--shape", default="reddit")
+    ap.add_argument("--ld", default="0", help="X row strides to try (0 = F)")
+    args = ap.parse_args()
+    libs = [_lib.LIB_PATH] + [p for p in args.libs.split(",") if p]
+    loaded = [(os.path.basename(p), _lib.load_path(p)) for p in libs]
+    thresholds = [int(t) for t in args.thresholds.split(",")]
+
+    dev = torch.device("cuda", 0)
+    S = graphs.synthetic_graph(args.shape, seed=0)
+    F = graphs.SHAPES[args.shape]["features"]
+    X = torch.from_numpy(graphs.synthetic_features(args.shape, S.n, F, seed=1)).to(dev)
+    csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
+    plans = {t: csr.plan(0, S.n, t) for t in thresholds}
+    Y = torch.empty_like(X)
+    lds = [int(x) or F for x in args.ld.split(",")]
+    Xs = {}
+    for ld in lds:
+        buf = torch.zeros((S.n, ld), device=dev)
+        buf[:, :F] = X
+        Xs[ld] = buf
+    stream = _lib.stream_handle(dev)
+    ref = None
+    slices = [int(x) for x in args.slices.split(",")]
+    variants = [(f"{name}/s{sf}/ld{ld}", lib, t, (sf, ld)) for name, lib in loaded
+                for t in thresholds for sf in slices for ld in lds]
+
+    def run(lib, t, cfg):
+        sf, ld = cfg
+        lib.sgc_set_tuning(b"slice_floats", sf)
+        plan, nh, thr = plans[t]
+        rc = lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val),
+                                  0, S.n, _lib.ptr(Xs[ld]), ld, _lib.ptr(Y), F, F, _lib.ptr(plan),
+                                  nh, thr, stream)
+        if rc:
+            raise RuntimeError(lib.sgc_last_error())
+
+    times = {(n, t): [] for n, _, t, _ in variants}
+    for name, lib, t, sf in variants:  # warm-up + correctness
+        run(lib, t, sf)
+        torch.cuda.synchronize()
+        out = Y.cpu().numpy().view(np.uint32).copy()
+        if ref is None:
+            ref = out
+        elif not np.array_equal(ref, out):
+            raise SystemExit(f"variant {name} t={t} is NOT bit-identical")
+    for _ in range(args.rounds):
+        for name, lib, t, sf in variants:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(args.reps):
+                run(lib, t, sf)
+            e.record()
+            e.synchronize()
+            times[(name, t)].append(s.elapsed_time(e) / args.reps)
+    alg = 4 * (S.n + 1) + 8 * S.nnz + 4 * F * S.nnz + 4 * F * S.n
+    res = []
+    for (name, t), v in times.items():
+        med = float(np.median(v))
+        res.append({"lib": name, "threshold": t, "median_ms": round(med, 4),
+                    "min_ms": round(float(np.min(v)), 4), "gather_model_TBps": round(alg / med / 1e9, 3)})
+    res.sort(key=lambda r: r["median_ms"])
+    for r in res:
+        print(json.dumps(r))
+
+
+if __name__ == "__main__":
+    del ctypes
+    main()

@@ -20,6 +20,8 @@ _p, _sz = ctypes.c_void_p, ctypes.c_size_t
 SIGNATURES = {
     "sgc_abi_version": (ctypes.c_int, []),
     "sgc_last_error": (ctypes.c_char_p, []),
+    "sgc_set_tuning": (ctypes.c_int, [ctypes.c_char_p, _i64]),
+    "sgc_get_tuning": (_i64, [ctypes.c_char_p]),
     "sgc_coo_to_csr_workspace": (ctypes.c_int, [_i64, _i64, ctypes.POINTER(_sz)]),
     "sgc_coo_to_csr": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _p, _p, _p, _p, _sz,
                                       ctypes.POINTER(_u32), _p]),
@@ -29,8 +31,11 @@ SIGNATURES = {
     "sgc_plan_build": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, ctypes.POINTER(_i64), _p]),
     "sgc_spmm_csr_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
                                         _p, _i64, _i32, _p]),
-    "sgc_propagate_f32": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32,
-                                         _p, _i64, _i32, _p]),
+    "sgc_propagate_workspace": (_i64, [_i64, _i64, _i64, _i32]),
+    "sgc_propagate_f32": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _i32,
+                                         _p, _i64, _i32, _p, _i64, _p]),
+    "sgc_pad_rows_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i64, _p]),
+    "sgc_aligned_ld": (_i64, [_i64]),
     "sgc_linear_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
 }
 
@@ -42,25 +47,29 @@ class SGCError(RuntimeError):
     pass
 
 
-def load():
-    """Load and type the library (once).  Raises if it is absent."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def load_path(path):
+    """Load and type one build of the library (tuning scripts load several)."""
+    if not os.path.exists(path):
         raise SGCError(
-            f"sgc_amd: native library {LIB_PATH} not found; build it with "
+            f"sgc_amd: native library {path} not found; build it with "
             "`python -m sgc_amd.build` (hipcc --offload-arch=gfx950). "
             "There is no CPU fallback.")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     if lib.sgc_abi_version() != ABI_VERSION:
         raise SGCError(f"sgc_amd: ABI mismatch ({lib.sgc_abi_version()} != {ABI_VERSION})")
-    _lib = lib
     return lib
+
+
+def load():
+    """Load and type the product library (once).  Raises if it is absent."""
+    global _lib
+    if _lib is None:
+        _lib = load_path(LIB_PATH)
+    return _lib
 
 
 def check(rc, what):

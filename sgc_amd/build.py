@@ -40,17 +40,21 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not _stale():
+def build(force=False, verbose=True, out=None, defines=()):
+    """Compile the library; `out`/`defines` build tuning variants elsewhere."""
+    lib = out or LIB
+    if not force and out is None and not _stale():
         return LIB
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
-    tmp = LIB + ".tmp"
-    cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), "-I", CSRC, *srcs, "-o", tmp]
+    tmp = lib + ".tmp"
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-I", os.path.join(ROOT, "include"),
+           "-I", CSRC, *srcs, "-o", tmp]
     if verbose:
         print("[sgc_amd] " + " ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":

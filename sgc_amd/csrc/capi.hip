@@ -29,6 +29,8 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
                 int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
                 int64_t ldy, int64_t F, const int32_t *heavy_rows, int64_t n_heavy,
                 int32_t heavy_threshold, hipStream_t stream);
+int set_tuning(const char *key, int64_t value);
+int64_t get_tuning(const char *key);
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                       int64_t ldy, int64_t M, int64_t K, int64_t C, hipStream_t stream);
 
@@ -41,6 +43,10 @@ extern "C" {
 int sgc_abi_version(void) { return SGC_ABI_VERSION; }
 
 const char *sgc_last_error(void) { return g_err; }
+
+int sgc_set_tuning(const char *key, int64_t value) { return set_tuning(key, value); }
+
+int64_t sgc_get_tuning(const char *key) { return get_tuning(key); }
 
 int sgc_coo_to_csr_workspace(int64_t n_rows, int64_t nnz, size_t *bytes_host) {
     return coo_to_csr_workspace(n_rows, nnz, bytes_host);
@@ -78,31 +84,70 @@ int sgc_spmm_csr_f32(const int32_t *row_ptr, const int32_t *col_idx, const float
                        plan ? n_heavy : 0, heavy_threshold, as_stream(stream));
 }
 
+int64_t sgc_aligned_ld(int64_t F) { return F <= 0 ? 0 : (F + 31) / 32 * 32; }
+
+static bool needs_pad(int64_t ldx, const float *X0) {
+    return (ldx % 32) != 0 || (reinterpret_cast<uintptr_t>(X0) % 128) != 0;
+}
+
+int64_t sgc_propagate_workspace(int64_t n_rows, int64_t F, int64_t ldx, int32_t K) {
+    if (n_rows <= 0 || F <= 0 || K <= 0) return 0;
+    const int64_t buf = n_rows * sgc_aligned_ld(F) * 4 + 256;
+    (void)ldx;  // sized for the padded-input case (the pointer's alignment is unknown here)
+    return (K >= 2 ? 2 : 1) * buf + 256;
+}
+
+int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int64_t n_rows,
+                     int64_t F, void *stream) {
+    SGC_REQUIRE(src && dst && lds >= F && ldd >= F && n_rows >= 0 && F >= 0, SGC_EINVAL,
+                "pad_rows: bad arguments");
+    if (n_rows == 0 || F == 0) return SGC_OK;
+    SGC_HIP_CHECK(hipMemcpy2DAsync(dst, ldd * 4, src, lds * 4, F * 4, n_rows,
+                                   hipMemcpyDeviceToDevice, as_stream(stream)));
+    return SGC_OK;
+}
+
 int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                       int64_t n_rows, const float *X0, int64_t ldx, float *out, int64_t ldo,
-                      float *work, int64_t F, int32_t K, const int32_t *plan, int64_t n_heavy,
-                      int32_t heavy_threshold, void *stream) {
+                      int64_t F, int32_t K, const int32_t *plan, int64_t n_heavy,
+                      int32_t heavy_threshold, void *workspace, int64_t workspace_bytes,
+                      void *stream) {
     hipStream_t s = as_stream(stream);
     SGC_REQUIRE(K >= 0, SGC_EINVAL, "propagate: negative degree %d", K);
     SGC_REQUIRE(X0 && out, SGC_EINVAL, "propagate: null pointer");
-    SGC_REQUIRE(K <= 1 || work, SGC_EINVAL, "propagate: K=%d needs a work buffer", K);
-    if (K == 0) {
-        if (n_rows > 0 && F > 0)
-            SGC_HIP_CHECK(hipMemcpy2DAsync(out, ldo * 4, X0, ldx * 4, F * 4, n_rows,
-                                           hipMemcpyDeviceToDevice, s));
-        return SGC_OK;
-    }
+    SGC_REQUIRE(ldx >= F && ldo >= F && F >= 0 && n_rows >= 0, SGC_EINVAL, "propagate: bad shape");
+    if (K == 0)
+        return sgc_pad_rows_f32(X0, ldx, out, ldo, n_rows, F, stream);
+    if (n_rows == 0 || F == 0) return SGC_OK;
+    const int64_t need = sgc_propagate_workspace(n_rows, F, ldx, K);
+    SGC_REQUIRE(workspace_bytes >= need && (need == 0 || workspace), SGC_ENOMEM,
+                "propagate: workspace %lld < %lld bytes", (long long)workspace_bytes,
+                (long long)need);
+    const int64_t ldw = sgc_aligned_ld(F);
+    const int64_t buf_floats = (n_rows * ldw * 4 + 256) / 4;
+    uintptr_t base = (reinterpret_cast<uintptr_t>(workspace) + 255) & ~uintptr_t(255);
+    float *bufs[2] = {reinterpret_cast<float *>(base), reinterpret_cast<float *>(base) + buf_floats};
+
     const float *src = X0;
     int64_t lds = ldx;
+    int next = 0;
+    if (needs_pad(ldx, X0)) {  // 128-B aligned copy of X_0 (workspace buffer 0)
+        const int rc = sgc_pad_rows_f32(X0, ldx, bufs[0], ldw, n_rows, F, stream);
+        if (rc) return rc;
+        src = bufs[0];
+        lds = ldw;
+        next = 1;
+    }
     for (int h = 0; h < K; ++h) {
-        const bool to_out = ((K - 1 - h) & 1) == 0;
-        float *dst = to_out ? out : work;
-        const int64_t ldd = to_out ? ldo : F;
+        const bool last = h == K - 1;
+        float *dst = last ? out : bufs[next];
+        const int64_t ldd = last ? ldo : ldw;
         const int rc = launch_spmm(row_ptr, col_idx, val, 0, n_rows, src, lds, dst, ldd, F, plan,
                                    plan ? n_heavy : 0, heavy_threshold, s);
         if (rc) return rc;
         src = dst;
         lds = ldd;
+        next ^= 1;
     }
     return SGC_OK;
 }

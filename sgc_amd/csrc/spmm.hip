@@ -8,18 +8,19 @@
 // or launches.
 //
 // Mapping (one wavefront = 64 lanes per work item):
-//   * light item = one whole row: lane l owns the V-float vectors at
-//     features (chunk0 + c)*64V + l*V, c in [0, C): C*V accumulators/lane.
-//     Y row reads of X are 64V-float coalesced segments of one X row.
-//   * heavy item = one (row, chunk) pair of a row with > heavy_threshold
-//     nonzeros: the row is split into its chunks_total feature chunks so a
-//     power-law hub runs on chunks_total waves at once (still one FMA chain
-//     per element).  Heavy items come first in the grid, sorted by degree
-//     (sgc_plan_build), so hubs start at t=0 and overlap the light rows.
+//   * features are cut into slices of 64*C*V floats (grid y); each slice is
+//     a complete pass over S, so the live part of X is N x slice floats (see
+//     the kernel comment: Infinity Cache / L2 residency);
+//   * light item = one row of one slice: lane l owns the V-float vectors at
+//     features (slice*C + c)*64V + l*V, c in [0, C): C*V accumulators/lane;
+//     each nonzero's X row segment is read as 64V-float coalesced loads;
+//   * heavy item = one 64-float sub-chunk of a row with > heavy_threshold
+//     nonzeros: power-law hubs run on 2..C*V waves per slice with UH nonzeros
+//     in flight each, scheduled first in their slice (sgc_plan_build sorts
+//     them by degree), still one FMA chain per element;
 //   * (col, val) of 64 consecutive nonzeros are read with one coalesced
-//     256-B load each, then broadcast per nonzero with v_readlane into SGPRs:
-//     the X row base address is scalar, each lane adds its fixed byte offset
-//     (global_load_dwordx{1,2,4} saddr + voffset).
+//     256-B load each, then broadcast per nonzero with v_readlane into SGPRs,
+//     so the X row base address is wave-uniform;
 //   * U nonzeros are in flight per wave before their FMAs (U*C*V registers);
 //     TLP (up to 8 waves/SIMD) hides the rest of the HBM/MALL latency.
 //
@@ -28,6 +29,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <string>
 #include <vector>
 
 namespace sgc {
@@ -65,40 +67,34 @@ __device__ __forceinline__ void row_chunks(const int *__restrict__ col,
             my_col = col[base + lane];
             my_val = val[base + lane];
         }
-        int j = 0;
-        for (; j + U <= n; j += U) {
+        // U nonzeros per step; the last step of a batch re-reads its last
+        // valid nonzero for the missing ones (same lines, no extra traffic)
+        // and skips their FMAs with a wave-uniform branch -- padding them
+        // with 0*x would turn a -0.0f accumulator into +0.0f.
+        for (int j = 0; j < n; j += U) {
             VT xv[U][C];
             float vv[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int cj = __builtin_amdgcn_readlane(my_col, j + u);
-                vv[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_val), j + u));
+                const int jj = min(j + u, n - 1);
+                const int cj = __builtin_amdgcn_readlane(my_col, jj);
+                vv[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_val), jj));
                 const char *xr = Xb + (int64_t)cj * row_bytes;
 #pragma unroll
                 for (int c = 0; c < C; ++c)
                     xv[u][c] = *reinterpret_cast<const VT *>(xr + boff[c]);
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u)
+            for (int u = 0; u < U; ++u) {
+                if (j + u < n) {
 #pragma unroll
-                for (int c = 0; c < C; ++c)
+                    for (int c = 0; c < C; ++c)
 #pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        set_elem<V>(acc[c], v,
-                                    __builtin_fmaf(vv[u], lane_elem<V>(xv[u][c], v),
-                                                   lane_elem<V>(acc[c], v)));
-        }
-        for (; j < n; ++j) {
-            const int cj = __builtin_amdgcn_readlane(my_col, j);
-            const float vj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_val), j));
-            const char *xr = Xb + (int64_t)cj * row_bytes;
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const VT x = *reinterpret_cast<const VT *>(xr + boff[c]);
-#pragma unroll
-                for (int v = 0; v < V; ++v)
-                    set_elem<V>(acc[c], v,
-                                __builtin_fmaf(vj, lane_elem<V>(x, v), lane_elem<V>(acc[c], v)));
+                        for (int v = 0; v < V; ++v)
+                            set_elem<V>(acc[c], v,
+                                        __builtin_fmaf(vv[u], lane_elem<V>(xv[u][c], v),
+                                                       lane_elem<V>(acc[c], v)));
+                }
             }
         }
     }
@@ -108,32 +104,46 @@ __device__ __forceinline__ void row_chunks(const int *__restrict__ col,
         if (ok[c]) *reinterpret_cast<VT *>(Yb + boff[c]) = acc[c];
 }
 
+// Grid: x = work items of one feature slice, y = slice.  Workgroups are
+// dispatched x-fastest, so the chip sweeps the slices one after another and
+// only X[:, slice] (N x 64CV floats -- 119 MB at Reddit shape for 128
+// floats) is live at a time: it stays in the 256 MB Infinity Cache and far
+// more of it in the 4 MB per-XCD L2s than whole 2.4 KB rows would.  Within a
+// slice the heavy rows come first (heaviest first), each split into
+// 64-float sub-chunks (dword loads, UH nonzeros in flight) so a power-law hub
+// is spread over 2C*V waves and finishes inside its slice.
+#ifndef SGC_HEAVY_VEC
+#define SGC_HEAVY_VEC 2
+#endif
 template <int V, int C, int U, int UH>
 __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
-    int row_begin, int n_rows, int F, const int *__restrict__ heavy_rows,
-    int n_heavy_items, int chunks_total, int heavy_threshold) {
+    int row_begin, int n_rows, int F, const int *__restrict__ heavy_rows, int n_heavy,
+    int heavy_threshold) {
+    constexpr int VH = (SGC_HEAVY_VEC < V) ? SGC_HEAVY_VEC : V;  // heavy lanes' vector width
+    constexpr int kSub = C * V / VH;  // 64*VH-float sub-chunks per slice (heavy items)
     const int lane = threadIdx.x & (kWave - 1);
-    const int64_t wave = __builtin_amdgcn_readfirstlane(
+    const int wave = __builtin_amdgcn_readfirstlane(
         (int)(blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave)));
+    const int slice = blockIdx.y;
+    const int n_heavy_items = n_heavy * kSub;
     if (wave < n_heavy_items) {
-        // heavy (row, chunk) item: only the first feature slice launches them
-        if (blockIdx.y != 0) return;
-        const int h = (int)wave / chunks_total;
-        const int c = (int)wave - h * chunks_total;
+        const int h = wave / kSub;
+        const int sub = slice * kSub + (wave - h * kSub);  // in units of 64*VH floats
+        if (sub * kWave * VH >= F) return;
         const int row = heavy_rows[h];
         const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
-        row_chunks<V, 1, UH>(col, val, k0, k1, X, ldx, Y + (int64_t)(row - row_begin) * ldy, F,
-                             c, lane);
+        row_chunks<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
+                                   Y + (int64_t)(row - row_begin) * ldy, F, sub, lane);
         return;
     }
-    const int64_t r = wave - n_heavy_items;
+    const int r = wave - n_heavy_items;
     if (r >= n_rows) return;
-    const int row = row_begin + (int)r;
+    const int row = row_begin + r;
     const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
-    if (heavy_rows != nullptr && k1 - k0 > heavy_threshold) return;  // done as heavy items
-    row_chunks<V, C, U>(col, val, k0, k1, X, ldx, Y + r * ldy, F, blockIdx.y * C, lane);
+    if (n_heavy > 0 && k1 - k0 > heavy_threshold) return;  // done as heavy items
+    row_chunks<V, C, U>(col, val, k0, k1, X, ldx, Y + (int64_t)r * ldy, F, slice * C, lane);
 }
 
 namespace {
@@ -151,21 +161,31 @@ struct LaunchArgs {
     int64_t ldy;
     int row_begin, n_rows, F;
     const int *heavy_rows;
-    int n_heavy_items, chunks_total, heavy_threshold;
+    int n_heavy, heavy_threshold;
     int slices;
     hipStream_t stream;
 };
 
+// Nonzeros in flight per wave: light items keep U*C*V <= ~40 registers of
+// gathered X; heavy sub-chunk items (one float per lane) go deeper (UH).
+#ifndef SGC_LIGHT_U_SCALE
+#define SGC_LIGHT_U_SCALE 2
+#endif
+#ifndef SGC_HEAVY_U
+#define SGC_HEAVY_U 32
+#endif
 template <int V, int C>
 hipError_t launch_vc(const LaunchArgs &a) {
-    constexpr int U = (C * V >= 16) ? 2 : (C * V >= 8) ? 4 : 8;
-    constexpr int UH = (V == 4) ? 8 : 16;
-    const int64_t waves = (int64_t)a.n_heavy_items + a.n_rows;
+    constexpr int U0 = (C * V >= 16) ? 2 : (C * V >= 8) ? 4 : 8;
+    constexpr int U = U0 * SGC_LIGHT_U_SCALE > 0 ? U0 * SGC_LIGHT_U_SCALE : 1;
+    constexpr int UH = SGC_HEAVY_U;
+    constexpr int VH = (SGC_HEAVY_VEC < V) ? SGC_HEAVY_VEC : V;
+    const int64_t waves = (int64_t)a.n_heavy * (C * V / VH) + a.n_rows;
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     dim3 grid((unsigned)blocks, (unsigned)a.slices);
     hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin, a.n_rows,
-                       a.F, a.heavy_rows, a.n_heavy_items, a.chunks_total, a.heavy_threshold);
+                       a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold);
     return hipGetLastError();
 }
 
@@ -179,10 +199,12 @@ hipError_t dispatch_c(int c, const LaunchArgs &a) {
     }
 }
 
+static int g_max_vec = 4;
+
 // Largest per-lane register vector the strides and base pointers allow.
 int pick_vec(int64_t F, int64_t ldx, int64_t ldy, const void *X, const void *Y) {
     for (int V : {4, 2}) {
-        if (F % V == 0 && ldx % V == 0 && ldy % V == 0 &&
+        if (V <= g_max_vec && F % V == 0 && ldx % V == 0 && ldy % V == 0 &&
             reinterpret_cast<uintptr_t>(X) % (4 * V) == 0 &&
             reinterpret_cast<uintptr_t>(Y) % (4 * V) == 0)
             return V;
@@ -193,6 +215,32 @@ int pick_vec(int64_t F, int64_t ldx, int64_t ldy, const void *X, const void *Y) 
 constexpr int max_chunks(int V) { return 16 / V; }  // <= 16 accumulators per lane
 
 }  // namespace
+
+// Slice width in 64V-float chunks; 0 = widest the registers allow (one
+// slice for F <= 64*16).  Set through sgc_set_tuning("slice_floats", n).
+static int g_slice_floats = 0;
+
+int set_tuning(const char *key, int64_t value) {
+    SGC_REQUIRE(key, SGC_EINVAL, "set_tuning: null key");
+    if (std::string(key) == "slice_floats") {
+        SGC_REQUIRE(value >= 0 && value < (1 << 20), SGC_EINVAL, "slice_floats out of range");
+        g_slice_floats = (int)value;
+        return SGC_OK;
+    }
+    if (std::string(key) == "max_vec") {
+        SGC_REQUIRE(value == 1 || value == 2 || value == 4, SGC_EINVAL, "max_vec must be 1, 2 or 4");
+        g_max_vec = (int)value;
+        return SGC_OK;
+    }
+    set_error("set_tuning: unknown key '%s'", key);
+    return SGC_EINVAL;
+}
+
+int64_t get_tuning(const char *key) {
+    if (key && std::string(key) == "slice_floats") return g_slice_floats;
+    if (key && std::string(key) == "max_vec") return g_max_vec;
+    return -1;
+}
 
 int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                 int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
@@ -207,17 +255,20 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     SGC_REQUIRE(n_heavy >= 0 && (n_heavy == 0 || heavy_rows), SGC_EINVAL, "spmm: bad plan");
     const int64_t n_rows = row_end - row_begin;
     if (n_rows == 0) return SGC_OK;
+    if (!heavy_rows) n_heavy = 0;
 
     const int V = pick_vec(F, ldx, ldy, X, Y);
     const int chunks_total = (int)((F + kWave * V - 1) / (kWave * V));
     const int cmax = max_chunks(V);
-    const int slices = (chunks_total + cmax - 1) / cmax;
-    const int C = (chunks_total + slices - 1) / slices;
-    const int64_t n_heavy_items = heavy_rows ? n_heavy * chunks_total : 0;
-    SGC_REQUIRE(n_heavy_items + n_rows < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many items");
+    int C = g_slice_floats > 0 ? std::max(1, g_slice_floats / (kWave * V)) : cmax;
+    C = std::min(C, std::min(cmax, chunks_total));
+    const int slices = (chunks_total + C - 1) / C;
+    const int64_t waves = n_heavy * (int64_t)C * V + n_rows;  // upper bound (VH >= 1)
+    SGC_REQUIRE(waves < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many work items");
+    SGC_REQUIRE(slices < 65536, SGC_ERANGE, "spmm: too many feature slices");
 
     LaunchArgs a{row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)n_rows, (int)F,
-                 heavy_rows, (int)n_heavy_items, chunks_total, heavy_threshold, slices, stream};
+                 heavy_rows, (int)n_heavy, heavy_threshold, slices, stream};
     hipError_t e;
     if (V == 4)
         e = dispatch_c<4, max_chunks(4)>(C, a);

@@ -7,7 +7,8 @@ unbalance the ranks, and computes those rows of X_{k+1} with the same HIP
 kernel (sgc_spmm_csr_f32 over a row range).  Between hops every rank needs
 all of X_k (at Reddit/RMAT shape nearly every column is referenced by every
 row block), so the exchange is one all-gather of the row blocks per hop --
-RCCL over xGMI with the "nccl" backend; gloo in the CPU tests.
+RCCL over xGMI with the "nccl" backend; gloo in the CPU tests.  The exchange
+is pipelined against the SpMM by feature groups (RowPartitionedPropagator).
 
 Layout trick: blocks are padded to the largest block (all_gather_into_tensor
 needs equal sizes) and the local CSR's column indices are remapped ONCE to
@@ -99,21 +100,39 @@ class RowPartitionedPropagator:
 
     X_0 must be the full [N, F] features on every rank (inputs replicated, as
     the reference loads them); the result is the full X_K on every rank.
-    `spmm_fn(shard, col_idx, X, out)` computes the rank's rows; the default is
-    the HIP kernel (tests inject the CPU oracle to exercise the exchange
-    logic over gloo)."""
 
-    def __init__(self, shard: ShardCSR, group=None, spmm_fn: Optional[Callable] = None):
+    Communication/compute overlap: features are processed in groups of
+    `group_floats` columns (independent FMA chains, so any grouping is
+    bit-exact).  For each hop, group g's local SpMM is followed by an
+    asynchronous all-gather of that group (RCCL runs on its own stream), so
+    the exchange of group g overlaps the SpMM of group g+1, and the next hop's
+    group g only waits for its own gather.  `spmm_fn(shard, col_idx, X, out)`
+    computes the rank's rows; the default is the HIP kernel (tests inject the
+    CPU oracle to exercise the exchange logic over gloo)."""
+
+    def __init__(self, shard: ShardCSR, group=None, spmm_fn: Optional[Callable] = None,
+                 group_floats: int = 128, host_staging: bool = False):
         self.shard = shard
         self.group = group
         self.spmm_fn = spmm_fn or _default_spmm
+        self.group_floats = max(2, int(group_floats) // 2 * 2)  # keep 8-B aligned groups
+        # rehearsal only: gather device buffers through host copies (gloo)
+        self.host_staging = host_staging
         self._bufs = {}
 
-    def _buf(self, name, shape, like):
-        b = self._bufs.get(name)
-        if b is None or b.shape != shape or b.device != like.device:
+    def _all_gather(self, dst, loc):
+        if not self.host_staging:
+            return dist.all_gather_into_tensor(dst, loc, group=self.group, async_op=True)
+        h_dst = torch.empty(dst.shape, dtype=dst.dtype)
+        dist.all_gather_into_tensor(h_dst, loc.cpu(), group=self.group)
+        dst.copy_(h_dst)
+        return None
+
+    def _buf(self, key, shape, like):
+        b = self._bufs.get(key)
+        if b is None or tuple(b.shape) != tuple(shape) or b.device != like.device:
             b = torch.empty(shape, dtype=torch.float32, device=like.device)
-            self._bufs[name] = b
+            self._bufs[key] = b
         return b
 
     def local_hop(self, X, padded_input, out):
@@ -126,17 +145,39 @@ class RowPartitionedPropagator:
         F = X0.shape[1]
         if K <= 0:
             return X0
-        gathered = [self._buf("g0", (P * B, F), X0), self._buf("g1", (P * B, F), X0)]
-        local = self._buf("local", (B, F), X0)
-        src, padded = X0, False
+        groups = [(a, min(F, a + self.group_floats)) for a in range(0, F, self.group_floats)]
+        if X0.is_cuda:
+            from .propagate import aligned_ld, _needs_pad
+            if _needs_pad(X0):  # 128-B aligned rows for hop 1's gathers (as propagate())
+                from . import _lib
+                Xa = self._buf("x0_aligned", (X0.shape[0], aligned_ld(F)), X0)
+                _lib.check(_lib.load().sgc_pad_rows_f32(
+                    _lib.ptr(X0), X0.stride(0), _lib.ptr(Xa), Xa.stride(0), X0.shape[0], F,
+                    _lib.stream_handle(X0.device)), "pad_rows_f32")
+                X0 = Xa[:, :F]
+        src = [X0[:, a:b] for a, b in groups]
+        padded = False
+        works = [None] * len(groups)
         for h in range(K):
-            self.local_hop(src, padded, local[:s.rows])
-            dst = gathered[h & 1]
-            dist.all_gather_into_tensor(dst, local, group=self.group)
-            src, padded = dst, True
+            par = h & 1
+            new_works, gathered = [], []
+            for gi, (a, b) in enumerate(groups):
+                if works[gi] is not None:
+                    works[gi].wait()  # this hop's input group has arrived (stream wait)
+                loc = self._buf(("local", par, gi), (B, b - a), X0)
+                self.local_hop(src[gi], padded, loc[:s.rows])
+                dst = self._buf(("gathered", par, gi), (P * B, b - a), X0)
+                new_works.append(self._all_gather(dst, loc))
+                gathered.append(dst)
+            works, src, padded = new_works, gathered, True
+        for w in works:
+            if w is not None:
+                w.wait()
         if out is None:
             out = torch.empty((s.n, F), dtype=torch.float32, device=X0.device)
         for p in range(P):
             r0, r1 = int(s.bounds[p]), int(s.bounds[p + 1])
-            out[r0:r1].copy_(src[p * B:p * B + (r1 - r0)])
+            if r1 > r0:
+                for gi, (a, b) in enumerate(groups):
+                    out[r0:r1, a:b].copy_(src[gi][p * B:p * B + (r1 - r0)])
         return out

@@ -14,7 +14,7 @@ from . import _lib
 
 # Rows with more nonzeros than this are split into per-feature-chunk work
 # items and scheduled first (see sgc_plan_build).  Results never depend on it.
-DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SGC_AMD_HEAVY_THRESHOLD", "512"))
+DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SGC_AMD_HEAVY_THRESHOLD", "2048"))
 
 STATUS_ROWS_SORTED = 1
 STATUS_COLS_ASCENDING = 2
@@ -188,28 +188,67 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
     return out
 
 
-def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, work=None, use_plan=True,
-              threshold=None):
-    """X_K = S^K X on the device (K >= 1); asynchronous on the current stream."""
+def aligned_ld(F):
+    """Row stride (floats) of the engine's own feature buffers: 128-B rows."""
+    return (F + 31) // 32 * 32
+
+
+def _needs_pad(X):
+    return X.stride(0) % 32 != 0 or X.data_ptr() % 128 != 0
+
+
+def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, threshold=None,
+              hop_hook=None, native_loop=False):
+    """X_K = S^K X on the device (K >= 1); asynchronous on the current stream.
+
+    Mirrors sgc_propagate_f32: X is first re-laid into 128-B aligned rows when
+    its rows are not (one streaming copy; each gathered X segment then spans
+    the fewest 128-B lines), hops ping-pong between two aligned buffers, the
+    last hop writes the contiguous [N, F] result.  hop_hook(phase, h) is called
+    around each hop's launch ("start"/"end", for event timing).
+    native_loop=True runs the same loop inside the C ABI call instead."""
     X = _check_features(X, csr)
     if csr.n_rows != csr.n_cols:
         raise RuntimeError("sgc_amd: propagation needs a square adjacency")
     n, F = X.shape
     if out is None:
         out = torch.empty((n, F), dtype=torch.float32, device=X.device)
-    if K > 1 and work is None:
-        work = torch.empty((n, F), dtype=torch.float32, device=X.device)
-    if n == 0 or F == 0:
+    if n == 0 or F == 0 or K <= 0:
+        if K <= 0:
+            out.copy_(X)
         return out
     plan, n_heavy, thr = csr.plan(0, n, threshold) if use_plan else (None, 0, 0)
     lib = _lib.load()
+    stream = _lib.stream_handle(X.device)
+    ldw = aligned_ld(F)
     with torch.cuda.device(X.device):
-        _lib.check(lib.sgc_propagate_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
-                                         _lib.ptr(csr.val), n, _lib.ptr(X), X.stride(0),
-                                         _lib.ptr(out), out.stride(0),
-                                         _lib.ptr(work) if K > 1 else None, F, int(K),
-                                         _lib.ptr(plan), n_heavy, thr,
-                                         _lib.stream_handle(X.device)), "propagate_f32")
+        if native_loop:
+            ws_bytes = lib.sgc_propagate_workspace(n, F, X.stride(0), K)
+            ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8, device=X.device)
+            _lib.check(lib.sgc_propagate_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
+                                             _lib.ptr(csr.val), n, _lib.ptr(X), X.stride(0),
+                                             _lib.ptr(out), out.stride(0), F, int(K),
+                                             _lib.ptr(plan), n_heavy, thr, _lib.ptr(ws), ws_bytes,
+                                             stream), "propagate_f32")
+            return out
+        bufs = [torch.empty((n, ldw), dtype=torch.float32, device=X.device)
+                for _ in range(2 if K >= 2 else 1)]
+        src, nxt = X, 0
+        if _needs_pad(X):
+            _lib.check(lib.sgc_pad_rows_f32(_lib.ptr(X), X.stride(0), _lib.ptr(bufs[0]), ldw, n, F,
+                                            stream), "pad_rows_f32")
+            src, nxt = bufs[0][:, :F], 1 % len(bufs)
+        for h in range(K):
+            dst = out if h == K - 1 else bufs[nxt][:, :F]
+            if hop_hook:
+                hop_hook("start", h)
+            _lib.check(lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
+                                            _lib.ptr(csr.val), 0, n, _lib.ptr(src), src.stride(0),
+                                            _lib.ptr(dst), dst.stride(0), F, _lib.ptr(plan),
+                                            n_heavy, thr, stream), "spmm_csr_f32")
+            if hop_hook:
+                hop_hook("end", h)
+            src, nxt = dst, nxt ^ 1
     return out
 
 

@@ -43,7 +43,7 @@ def _oracle_spmm(shard, col, X, out):
     return out
 
 
-def _worker(rank, world, port, case, K, result_q):
+def _worker(rank, world, port, case, K, result_q, group_floats=128, staging=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -51,7 +51,8 @@ def _worker(rank, world, port, case, K, result_q):
         n = int(case["n"])
         rp, ci, va = o.coo_to_csr(n, n, case["rows"], case["cols"], case["vals"])
         shard = make_shard(rp, ci, va, rank, world, "cpu")
-        prop = RowPartitionedPropagator(shard, spmm_fn=_oracle_spmm)
+        prop = RowPartitionedPropagator(shard, spmm_fn=_oracle_spmm, group_floats=group_floats,
+                                        host_staging=staging)
         X0 = torch.from_numpy(case["X"])
         out = prop.propagate(X0, K)
         result_q.put((rank, out.numpy()))
@@ -59,15 +60,17 @@ def _worker(rank, world, port, case, K, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,name,K", [(2, "norm_n48_F65", 2), (2, "hub1000_F65", 2),
-                                          (3, "norm_n48_F602", 3), (4, "raw_unsorted_dups_F7", 3),
-                                          (2, "isolated_F17", 1)])
-def test_row_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K):
+@pytest.mark.parametrize("world,name,K,gf,staging", [
+    (2, "norm_n48_F65", 2, 128, False), (2, "hub1000_F65", 2, 16, False),
+    (3, "norm_n48_F602", 3, 128, False), (4, "raw_unsorted_dups_F7", 3, 2, False),
+    (2, "isolated_F17", 1, 4, True), (2, "norm_n48_F130", 2, 64, True)])
+def test_row_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, gf, staging):
     case = tiny_cases[name]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, K, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, K, q, gf, staging))
+             for r in range(world)]
     for p in procs:
         p.start()
     results = dict(q.get(timeout=120) for _ in range(world))

@@ -77,6 +77,23 @@ def test_no_plan_path(tiny_cases):
     assert bits_equal(out.cpu().numpy(), c["Y2"])
 
 
+@pytest.mark.parametrize("native", [False, True])
+@pytest.mark.parametrize("ld_extra", [0, 38, 3])
+def test_propagate_layouts_and_native_loop(tiny_cases, native, ld_extra):
+    """Python hop loop and the C ABI loop (sgc_propagate_f32), with inputs
+    needing the 128-B re-layout (ld 602 / 605) and not (ld 640)."""
+    from sgc_amd.propagate import DeviceCSR, propagate
+    c = tiny_cases["norm_n48_F602"]
+    csr = DeviceCSR.from_torch(coo_cuda(c))
+    X = torch.from_numpy(c["X"]).to(DEV)
+    buf = torch.full((X.shape[0], 602 + ld_extra), float("nan"), device=DEV)
+    buf[:, :602] = X
+    for K in (0, 1, 2, 3):
+        out = propagate(csr, buf[:, :602], K, native_loop=native)
+        torch.cuda.synchronize()
+        assert bits_equal(out.cpu().numpy(), c[f"Y{K}"]), (K, native, ld_extra)
+
+
 def test_row_slices_and_strides(tiny_cases):
     """Row-range SpMM (the multi-GPU shard kernel) + padded strides."""
     from sgc_amd.propagate import DeviceCSR, spmm
