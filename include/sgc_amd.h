@@ -77,6 +77,35 @@ int sgc_csr64_to_csr(const int64_t *crow, const int64_t *col, const float *vals,
                      uint32_t *status_host, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * On-device augmented normalisation S = D^-1/2 (A+I) D^-1/2 (reference
+ * normalization.py:5-12 + the fp32 rounding of utils.py:25), bit-exact with
+ * scipy's result.  A: canonical CSR (ascending unique columns per row), fp64
+ * values.  Two passes around one host step, exactly as the reference splits
+ * its arithmetic:
+ *   1. sgc_augnorm_count: per-row entry count of A+I -> out_row_ptr (scan) and
+ *      rowsum (fp64, sequential in column order); *out_nnz_host = nnz(S).
+ *      Synchronous.  Returns SGC_EINVAL if A is not canonical.
+ *   2. host: d = rowsum ** -0.5, inf -> 0 (numpy, as normalization.py:8-10);
+ *   3. sgc_augnorm_fill: S entries (d_i * a_ij) * d_j in fp64 -> fp32, in
+ *      ascending column order, dropping exact zeros like scipy's csr_matmat
+ *      (out_row_ptr may shrink then; *out_nnz_host = final nnz).  Synchronous.
+ * workspace: sgc_augnorm_workspace(n) bytes of device scratch.
+ * ------------------------------------------------------------------------- */
+int64_t sgc_augnorm_workspace(int64_t n_rows);
+int sgc_augnorm_count(const int32_t *row_ptr, const int32_t *col_idx, const double *val,
+                      int64_t n_rows, int64_t nnz, int32_t *out_row_ptr, double *rowsum,
+                      void *workspace, int64_t workspace_bytes, int64_t *out_nnz_host,
+                      uint32_t *status_host, void *stream);
+int sgc_augnorm_fill(const int32_t *row_ptr, const int32_t *col_idx, const double *val,
+                     int64_t n_rows, const double *d, int32_t *out_row_ptr,
+                     int32_t *out_col_idx, float *out_val, void *workspace,
+                     int64_t workspace_bytes, int64_t *out_nnz_host, void *stream);
+
+/* CSR -> torch COO indices: rows64[k], cols64[k] (int64) of every entry. */
+int sgc_csr_to_coo64(const int32_t *row_ptr, const int32_t *col_idx, int64_t n_rows,
+                     int64_t *rows64, int64_t *cols64, void *stream);
+
+/* ---------------------------------------------------------------------------
  * Schedule ("plan") for the SpMM.  Lists the rows of [row_begin, row_end)
  * with more than heavy_threshold nonzeros, heaviest first.  sgc_spmm_csr_f32
  * runs each listed row as one work item per 64V-float feature chunk (so a

@@ -27,6 +27,12 @@ SIGNATURES = {
                                       ctypes.POINTER(_u32), _p]),
     "sgc_csr64_to_csr": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _p, _p, _p,
                                         ctypes.POINTER(_u32), _p]),
+    "sgc_augnorm_workspace": (_i64, [_i64]),
+    "sgc_augnorm_count": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _p, _p, _i64,
+                                         ctypes.POINTER(_i64), ctypes.POINTER(_u32), _p]),
+    "sgc_augnorm_fill": (ctypes.c_int, [_p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64,
+                                        ctypes.POINTER(_i64), _p]),
+    "sgc_csr_to_coo64": (ctypes.c_int, [_p, _p, _i64, _p, _p, _p]),
     "sgc_plan_capacity": (_i64, [_i64]),
     "sgc_plan_build": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, ctypes.POINTER(_i64), _p]),
     "sgc_spmm_csr_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,

@@ -29,6 +29,17 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
                 int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
                 int64_t ldy, int64_t F, const int32_t *heavy_rows, int64_t n_heavy,
                 int32_t heavy_threshold, hipStream_t stream);
+int launch_pad_rows(const float *src, int64_t lds, float *dst, int64_t ldd, int64_t n_rows,
+                    int64_t F, hipStream_t stream);
+size_t augnorm_scan_temp_bytes(int64_t n);
+int augnorm_count(const int32_t *row_ptr, const int32_t *col, const double *val, int64_t n,
+                  int64_t nnz, int32_t *out_row_ptr, double *rowsum, void *ws, size_t ws_bytes,
+                  int64_t *out_nnz_host, uint32_t *status_host, hipStream_t s);
+int augnorm_fill(const int32_t *row_ptr, const int32_t *col, const double *val, int64_t n,
+                 const double *d, int32_t *out_row_ptr, int32_t *out_col, float *out_val,
+                 void *ws, size_t ws_bytes, int64_t *out_nnz_host, hipStream_t s);
+int csr_to_coo64(const int32_t *row_ptr, const int32_t *col, int64_t n, int64_t *rows64,
+                 int64_t *cols64, hipStream_t s);
 int set_tuning(const char *key, int64_t value);
 int64_t get_tuning(const char *key);
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
@@ -67,6 +78,36 @@ int sgc_csr64_to_csr(const int64_t *crow, const int64_t *col, const float *vals,
                         status_host, as_stream(stream));
 }
 
+int64_t sgc_augnorm_workspace(int64_t n_rows) {
+    const int64_t n = n_rows < 1 ? 1 : n_rows;
+    return 4 * ((n * 4 + 255) / 256 * 256) + (int64_t)augnorm_scan_temp_bytes(n) + 1024;
+}
+
+int sgc_augnorm_count(const int32_t *row_ptr, const int32_t *col_idx, const double *val,
+                      int64_t n_rows, int64_t nnz, int32_t *out_row_ptr, double *rowsum,
+                      void *workspace, int64_t workspace_bytes, int64_t *out_nnz_host,
+                      uint32_t *status_host, void *stream) {
+    SGC_REQUIRE(out_nnz_host, SGC_EINVAL, "augnorm_count: null out_nnz_host");
+    return augnorm_count(row_ptr, col_idx, val, n_rows, nnz, out_row_ptr, rowsum, workspace,
+                         workspace_bytes < 0 ? 0 : (size_t)workspace_bytes, out_nnz_host,
+                         status_host, as_stream(stream));
+}
+
+int sgc_augnorm_fill(const int32_t *row_ptr, const int32_t *col_idx, const double *val,
+                     int64_t n_rows, const double *d, int32_t *out_row_ptr, int32_t *out_col_idx,
+                     float *out_val, void *workspace, int64_t workspace_bytes,
+                     int64_t *out_nnz_host, void *stream) {
+    SGC_REQUIRE(out_nnz_host, SGC_EINVAL, "augnorm_fill: null out_nnz_host");
+    return augnorm_fill(row_ptr, col_idx, val, n_rows, d, out_row_ptr, out_col_idx, out_val,
+                        workspace, workspace_bytes < 0 ? 0 : (size_t)workspace_bytes,
+                        out_nnz_host, as_stream(stream));
+}
+
+int sgc_csr_to_coo64(const int32_t *row_ptr, const int32_t *col_idx, int64_t n_rows,
+                     int64_t *rows64, int64_t *cols64, void *stream) {
+    return csr_to_coo64(row_ptr, col_idx, n_rows, rows64, cols64, as_stream(stream));
+}
+
 int64_t sgc_plan_capacity(int64_t n_rows) { return 2 * (n_rows < 0 ? 0 : n_rows) + 1; }
 
 int sgc_plan_build(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
@@ -99,12 +140,7 @@ int64_t sgc_propagate_workspace(int64_t n_rows, int64_t F, int64_t ldx, int32_t 
 
 int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int64_t n_rows,
                      int64_t F, void *stream) {
-    SGC_REQUIRE(src && dst && lds >= F && ldd >= F && n_rows >= 0 && F >= 0, SGC_EINVAL,
-                "pad_rows: bad arguments");
-    if (n_rows == 0 || F == 0) return SGC_OK;
-    SGC_HIP_CHECK(hipMemcpy2DAsync(dst, ldd * 4, src, lds * 4, F * 4, n_rows,
-                                   hipMemcpyDeviceToDevice, as_stream(stream)));
-    return SGC_OK;
+    return launch_pad_rows(src, lds, dst, ldd, n_rows, F, as_stream(stream));
 }
 
 int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,

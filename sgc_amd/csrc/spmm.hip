@@ -281,6 +281,44 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
 }
 
 // ---------------------------------------------------------------------------
+// Row re-layout dst[i, 0:F] = src[i, 0:F]: one wave per row, V-float vectors
+// (the runtime's 2-D copy blit reached only ~3 TB/s on this shape).
+template <int V>
+__global__ __launch_bounds__(256) void pad_rows_kernel(const float *__restrict__ src, int64_t lds,
+                                                      float *__restrict__ dst, int64_t ldd,
+                                                      int64_t n_rows, int F) {
+    using VT = typename Vec<V>::T;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t waves = (int64_t)gridDim.x * (blockDim.x / kWave);
+    for (int64_t r = blockIdx.x * (int64_t)(blockDim.x / kWave) + threadIdx.x / kWave; r < n_rows;
+         r += waves) {
+        const VT *s = reinterpret_cast<const VT *>(src + r * lds);
+        VT *d = reinterpret_cast<VT *>(dst + r * ldd);
+        for (int i = lane; i < F / V; i += kWave) d[i] = s[i];
+    }
+}
+
+int launch_pad_rows(const float *src, int64_t lds, float *dst, int64_t ldd, int64_t n_rows,
+                    int64_t F, hipStream_t stream) {
+    SGC_REQUIRE(src && dst && lds >= F && ldd >= F && n_rows >= 0 && F >= 0 && F < INT32_MAX,
+                SGC_EINVAL, "pad_rows: bad arguments");
+    if (n_rows == 0 || F == 0) return SGC_OK;
+    const int64_t blocks = std::min<int64_t>((n_rows + 3) / 4, 256 * 16);
+    const int V = pick_vec(F, lds, ldd, src, dst);
+    if (V == 4)
+        hipLaunchKernelGGL(pad_rows_kernel<4>, dim3(blocks), dim3(256), 0, stream, src, lds, dst,
+                           ldd, n_rows, (int)F);
+    else if (V == 2)
+        hipLaunchKernelGGL(pad_rows_kernel<2>, dim3(blocks), dim3(256), 0, stream, src, lds, dst,
+                           ldd, n_rows, (int)F);
+    else
+        hipLaunchKernelGGL(pad_rows_kernel<1>, dim3(blocks), dim3(256), 0, stream, src, lds, dst,
+                           ldd, n_rows, (int)F);
+    SGC_HIP_CHECK(hipGetLastError());
+    return SGC_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Plan: list the rows with > threshold nonzeros, heaviest first.
 __global__ void heavy_rows_kernel(const int *__restrict__ row_ptr, int row_begin, int n_rows,
                                   int threshold, int *__restrict__ out_pairs,

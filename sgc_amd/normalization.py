@@ -50,3 +50,55 @@ def row_normalize(mx):
     # keep the row sums' dtype (float32 features stay float32, as the reference's)
     r_inv = _inv_power(np.asarray(mx.sum(1)).ravel(), -1)
     return sp.diags(r_inv).dot(mx)
+
+
+def aug_normalize_on_device(adj, device="cuda"):
+    """S = AugNorm(A) computed on the GPU (libsgc_amd: sgc_augnorm_count/fill),
+    bit-identical to aug_normalized_adjacency(A) -> fp32.  Returns a
+    sgc_amd.propagate.DeviceCSR ready for propagation.
+
+    A must be canonical CSR (scipy's has_canonical_format: sorted, unique
+    columns), which is what the loaders produce (networkx adjacency, A + A^T).
+    The only host step is the one the reference itself does in numpy:
+    d = rowsum ** -0.5 with inf -> 0 (normalization.py:8-10)."""
+    import torch
+
+    from . import _lib
+    from .propagate import DeviceCSR, ctypes_byref
+    a = sp.csr_matrix(adj)
+    if not a.has_canonical_format:
+        raise ValueError("aug_normalize_on_device: A must be canonical CSR "
+                         "(sorted unique column indices); use aug_normalized_adjacency")
+    n = a.shape[0]
+    if a.shape[0] != a.shape[1]:
+        raise ValueError("aug_normalize_on_device: A must be square")
+    if n >= 2**31 - 1 or a.nnz >= 2**31 - 1:
+        raise ValueError("aug_normalize_on_device: beyond int32 CSR")
+    dev = torch.device(device)
+    lib = _lib.load()
+    rp = torch.from_numpy(a.indptr.astype(np.int32)).to(dev)
+    ci = torch.from_numpy(a.indices.astype(np.int32)).to(dev)
+    va = torch.from_numpy(a.data.astype(np.float64)).to(dev)
+    out_rp = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    rowsum = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+    ws_bytes = lib.sgc_augnorm_workspace(n)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    nnz_out, status = _lib._i64(0), _lib._u32(0)
+    with torch.cuda.device(dev):
+        stream = _lib.stream_handle(dev)
+        _lib.check(lib.sgc_augnorm_count(_lib.ptr(rp), _lib.ptr(ci), _lib.ptr(va), n, a.nnz,
+                                         _lib.ptr(out_rp), _lib.ptr(rowsum), _lib.ptr(ws), ws_bytes,
+                                         ctypes_byref(nnz_out), ctypes_byref(status), stream),
+                   "augnorm_count")
+        d = torch.from_numpy(_inv_power(rowsum[:n].cpu().numpy(), -0.5)).to(dev)
+        total = int(nnz_out.value)
+        out_ci = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+        out_va = torch.empty(max(total, 1), dtype=torch.float32, device=dev)
+        _lib.check(lib.sgc_augnorm_fill(_lib.ptr(rp), _lib.ptr(ci), _lib.ptr(va), n, _lib.ptr(d),
+                                        _lib.ptr(out_rp), _lib.ptr(out_ci), _lib.ptr(out_va),
+                                        _lib.ptr(ws), ws_bytes, ctypes_byref(nnz_out), stream),
+                   "augnorm_fill")
+    total = int(nnz_out.value)
+    csr = DeviceCSR(n, n, out_rp, out_ci[:total], out_va[:total])
+    csr.status = 1 | 2  # rows sorted, columns ascending (canonical A + I)
+    return csr

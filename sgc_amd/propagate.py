@@ -135,6 +135,25 @@ class DeviceCSR:
         return self._plans[key]
 
 
+def to_torch_coo(csr: DeviceCSR):
+    """torch sparse COO (int64 [2, nnz] indices, fp32 values, not coalesced) with
+    the entries in CSR order -- the tensor sparse_mx_to_torch_sparse_tensor
+    (utils.py:23-30) builds -- with `csr` attached as its propagation cache."""
+    lib = _lib.load()
+    nnz = csr.nnz
+    idx = torch.empty((2, nnz), dtype=torch.int64, device=csr.device)
+    with torch.cuda.device(csr.device):
+        _lib.check(lib.sgc_csr_to_coo64(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), csr.n_rows,
+                                        _lib.ptr(idx[0]), _lib.ptr(idx[1]),
+                                        _lib.stream_handle(csr.device)), "csr_to_coo64")
+    adj = torch.sparse_coo_tensor(idx, csr.val, (csr.n_rows, csr.n_cols))
+    try:
+        adj._sgc_amd_csr = (adj._version, csr)
+    except (AttributeError, RuntimeError):
+        pass
+    return adj
+
+
 def ctypes_byref(x):
     import ctypes
     return ctypes.byref(x)

@@ -19,8 +19,8 @@ import numpy as np
 import scipy.sparse as sp
 import torch
 
-from .normalization import fetch_normalization, row_normalize
-from .propagate import csr_of, propagate
+from .normalization import aug_normalize_on_device, fetch_normalization, row_normalize
+from .propagate import csr_of, propagate, to_torch_coo
 
 
 def parse_index_file(filename):
@@ -41,6 +41,17 @@ def sparse_mx_to_torch_sparse_tensor(sparse_mx):
     indices = torch.from_numpy(np.stack([coo.row, coo.col]).astype(np.int64))
     values = torch.from_numpy(coo.data)
     return torch.sparse_coo_tensor(indices, values, torch.Size(coo.shape))
+
+
+def _normalized_adj(adj, normalization, cuda):
+    """The loaders' adjacency: AugNorm on the GPU when it applies (canonical A,
+    'AugNormAdj', cuda) -- bit-identical to the reference's host scipy path and
+    ~1000x faster at Reddit shape -- else the reference's host path."""
+    a = sp.csr_matrix(adj)
+    if cuda and normalization == "AugNormAdj" and a.has_canonical_format:
+        return to_torch_coo(aug_normalize_on_device(a, "cuda"))
+    t = sparse_mx_to_torch_sparse_tensor(fetch_normalization(normalization)(adj)).float()
+    return t.cuda() if cuda else t
 
 
 def sgc_precompute(features, adj, degree):
@@ -109,14 +120,14 @@ def load_citation(dataset_str="cora", normalization="AugNormAdj", cuda=True):
     idx_train = range(len(y))
     idx_val = range(len(y), len(y) + 500)
 
-    adj, features = preprocess_citation(adj, features, normalization)
+    features = row_normalize(features)
+    adj = _normalized_adj(adj, normalization, cuda)
 
     features = torch.FloatTensor(np.array(features.todense())).float()
     labels = torch.LongTensor(labels).max(dim=1)[1]
-    adj = sparse_mx_to_torch_sparse_tensor(adj).float()
     idx_train, idx_val, idx_test = (torch.LongTensor(i) for i in (idx_train, idx_val, idx_test))
     if cuda:
-        features, adj, labels = features.cuda(), adj.cuda(), labels.cuda()
+        features, labels = features.cuda(), labels.cuda()
         idx_train, idx_val, idx_test = idx_train.cuda(), idx_val.cuda(), idx_test.cuda()
     return adj, features, labels, idx_train, idx_val, idx_test
 
@@ -149,10 +160,9 @@ def load_reddit_data(data_path="data/", normalization="AugNormAdj", cuda=True):
     train_adj = adj[train_index, :][:, train_index]
     features = torch.FloatTensor(np.array(features))
     features = (features - features.mean(dim=0)) / features.std(dim=0)
-    normalizer = fetch_normalization(normalization)
-    adj = sparse_mx_to_torch_sparse_tensor(normalizer(adj)).float()
-    train_adj = sparse_mx_to_torch_sparse_tensor(normalizer(train_adj)).float()
+    adj = _normalized_adj(adj, normalization, cuda)
+    train_adj = _normalized_adj(train_adj, normalization, cuda)
     labels = torch.LongTensor(labels)
     if cuda:
-        adj, train_adj, features, labels = adj.cuda(), train_adj.cuda(), features.cuda(), labels.cuda()
+        features, labels = features.cuda(), labels.cuda()
     return adj, train_adj, features, labels, train_index, val_index, test_index
