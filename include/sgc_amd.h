@@ -169,6 +169,24 @@ int64_t sgc_aligned_ld(int64_t F);
 int sgc_linear_f32(const float *X, int64_t ldx, const float *W, const float *b,
                    float *Y, int64_t ldy, int64_t M, int64_t K, int64_t C, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Fused classifier training step: for the SGC closure
+ * (citation.py:46-49, reddit.py:55-58: F.cross_entropy(model(x), y) then
+ * backward) computes, in three launches reading X twice,
+ *     loss = mean_m [ logsumexp(z_m) - z_m[y_m] ],  z = X W^T + b
+ *     dW   = (softmax(z) - onehot(y))^T X / M,     db = sum_m (...) / M
+ * loss is one float; dW [C,K], db [C] (db may be NULL); logits [M,C] with row
+ * stride ldl are written when non-NULL.  C <= 64.  Labels must lie in
+ * [0, C) (not checked on the device).  Reductions run in a fixed order:
+ * results are bitwise reproducible run to run; within fp32 tolerance of torch.
+ * workspace: sgc_linear_xent_workspace(M, K, C) bytes.
+ * ------------------------------------------------------------------------- */
+int64_t sgc_linear_xent_workspace(int64_t M, int64_t K, int64_t C);
+int sgc_linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
+                        const int64_t *labels, int64_t M, int64_t K, int64_t C, float *loss,
+                        float *dW, float *db, float *logits, int64_t ldl, void *workspace,
+                        int64_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,6 +22,7 @@ for s in $STEPS; do
     pytest) run pytest timeout -k 10 900 python -m pytest tests -x -q -m gpu ;;
     smoke)  run smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench timeout -k 10 600 python bench.py ${BENCH_ARGS} ;;
+    aux)    run aux timeout -k 10 600 python scripts/bench_aux.py ;;
     dist)   run dist timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
                 --dist-backend gloo ;;

@@ -43,6 +43,9 @@ SIGNATURES = {
     "sgc_pad_rows_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i64, _p]),
     "sgc_aligned_ld": (_i64, [_i64]),
     "sgc_linear_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "sgc_linear_xent_workspace": (_i64, [_i64, _i64, _i64]),
+    "sgc_linear_xent_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _p, _p, _p,
+                                           _p, _i64, _p, _i64, _p]),
 }
 
 ABI_VERSION = 1

@@ -40,6 +40,11 @@ int augnorm_fill(const int32_t *row_ptr, const int32_t *col, const double *val, 
                  void *ws, size_t ws_bytes, int64_t *out_nnz_host, hipStream_t s);
 int csr_to_coo64(const int32_t *row_ptr, const int32_t *col, int64_t n, int64_t *rows64,
                  int64_t *cols64, hipStream_t s);
+int64_t xent_workspace_bytes(int64_t M, int64_t K, int64_t C);
+int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
+                    const int64_t *labels, int64_t M, int64_t K, int64_t C, float *loss,
+                    float *dW, float *db, float *logits, int64_t ldl, void *ws, int64_t ws_bytes,
+                    hipStream_t s);
 int set_tuning(const char *key, int64_t value);
 int64_t get_tuning(const char *key);
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
@@ -191,6 +196,18 @@ int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const floa
 int sgc_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                    int64_t ldy, int64_t M, int64_t K, int64_t C, void *stream) {
     return launch_linear_f32(X, ldx, W, b, Y, ldy, M, K, C, as_stream(stream));
+}
+
+int64_t sgc_linear_xent_workspace(int64_t M, int64_t K, int64_t C) {
+    return xent_workspace_bytes(M, K, C);
+}
+
+int sgc_linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
+                        const int64_t *labels, int64_t M, int64_t K, int64_t C, float *loss,
+                        float *dW, float *db, float *logits, int64_t ldl, void *workspace,
+                        int64_t workspace_bytes, void *stream) {
+    return linear_xent_f32(X, ldx, W, b, labels, M, K, C, loss, dW, db, logits, ldl, workspace,
+                           workspace_bytes, as_stream(stream));
 }
 
 }  // extern "C"

@@ -1,0 +1,363 @@
+// xent.hip -- fused SGC classifier training step on gfx950 (SURVEY.md 8(f)
+// row 2): loss = mean_m CE(softmax(x_m W^T + b), y_m) and its gradients
+// dW = G^T X / M, db = sum_m G_m / M with G = softmax - onehot -- what the
+// reference's closure computes through nn.Linear + F.cross_entropy +
+// backward (citation.py:47-49, reddit.py:55-58).
+//
+// Three launches, X read from HBM twice (the floor without keeping a
+// 2.4 KB-per-row tile on chip between the two GEMMs):
+//   A  xent_fwd_kernel    logits on fp32 MFMA (the linear_kernel mapping),
+//                         row softmax / log-sum-exp across the 16-lane class
+//                         groups (DPP shuffles), G -> global [M][C16] (fp32,
+//                         padded classes 0), per-wave loss and dG column sums;
+//   B  xent_dw_kernel     dW partial slabs: each block owns a contiguous run
+//                         of rows and reduces G^T X over them on MFMA
+//                         (A = G^T straight from G's row-major layout,
+//                         B = X rows, V-vector loads split over V MFMAs);
+//   C  xent_reduce_kernel slabs -> dW, per-wave partials -> db and loss, in a
+//                         fixed order (bitwise reproducible run to run).
+#include "common.h"
+
+namespace sgc {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+__device__ __forceinline__ float group16_max(float v) {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+    return v;
+}
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+// ---- A: logits -> G, loss / dG partials ------------------------------------
+template <int V, int MT, int NT>
+__global__ __launch_bounds__(256) void xent_fwd_kernel(
+    const float *__restrict__ X, int64_t ldx, const float *__restrict__ W,
+    const float *__restrict__ b, const int64_t *__restrict__ labels, int M, int K, int C,
+    float inv_m, float *__restrict__ G, int ldg, double *__restrict__ loss_part,
+    float *__restrict__ db_part, float *__restrict__ logits, int64_t ldl) {
+    using VT = typename Vec<V>::T;
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int m0 = wave * (MT * 16);
+    if (m0 >= M) return;  // the partial arrays hold exactly ceil(M / 16MT) waves
+    const int i = lane & 15, g = lane >> 4;
+    double wave_loss = 0.0;
+    float dbc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) dbc[n] = 0.f;
+    {
+        const float *xrow[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) xrow[t] = X + (int64_t)min(m0 + t * 16 + i, M - 1) * ldx;
+        const float *wrow[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) wrow[n] = W + (int64_t)min(n * 16 + i, C - 1) * K;
+        f32x4 acc[MT][NT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int k0 = 0; k0 < K; k0 += 4 * V) {
+            const int k = k0 + g * V;
+            const bool ok = k < K;
+            const int kk = ok ? k : 0;
+            VT xa[MT], wb[NT];
+#pragma unroll
+            for (int t = 0; t < MT; ++t) {
+                xa[t] = *reinterpret_cast<const VT *>(xrow[t] + kk);
+                if (!ok) xa[t] = VT{};
+            }
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                wb[n] = *reinterpret_cast<const VT *>(wrow[n] + kk);
+                if (!ok) wb[n] = VT{};
+            }
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+#pragma unroll
+                for (int t = 0; t < MT; ++t)
+#pragma unroll
+                    for (int n = 0; n < NT; ++n)
+                        acc[t][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            lane_elem<V>(xa[t], v), lane_elem<V>(wb[n], v), acc[t][n], 0, 0, 0);
+        }
+        float bias[NT];
+        bool valid[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int c = n * 16 + i;
+            valid[n] = c < C;
+            bias[n] = (valid[n] && b) ? b[c] : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + t * 16 + g * 4 + r;
+                const bool row_ok = m < M;  // wave-group uniform per (t, r, g)
+                float z[NT];
+                float mx = -INFINITY;
+#pragma unroll
+                for (int n = 0; n < NT; ++n) {
+                    z[n] = valid[n] ? acc[t][n][r] + bias[n] : -INFINITY;
+                    mx = fmaxf(mx, z[n]);
+                }
+                mx = group16_max(mx);
+                float se = 0.f;
+#pragma unroll
+                for (int n = 0; n < NT; ++n) se += valid[n] ? expf(z[n] - mx) : 0.f;
+                se = group16_sum(se);
+                const float lse = mx + logf(se);
+                const int64_t y = row_ok ? labels[m] : -1;
+                float zy = 0.f;
+#pragma unroll
+                for (int n = 0; n < NT; ++n) {
+                    const int c = n * 16 + i;
+                    const bool is_y = (c == y);
+                    if (is_y) zy = z[n];
+                    const float p = valid[n] ? expf(z[n] - lse) : 0.f;
+                    const float gv = row_ok ? (p - (is_y ? 1.f : 0.f)) * inv_m : 0.f;
+                    if (row_ok) {
+                        G[(int64_t)m * ldg + c] = gv;
+                        if (logits && valid[n]) logits[(int64_t)m * ldl + c] = z[n];
+                    }
+                    dbc[n] += gv;
+                }
+                zy = group16_sum(zy);  // exactly one lane of the group holds z_y
+                if (row_ok && i == 0) wave_loss += (double)(lse - zy);
+            }
+    }
+    // per-wave partials: loss (lanes i==0 of each group), dG column sums
+    double l = wave_loss;
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (lane == 0) loss_part[wave] = l;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+        float s = dbc[n];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (g == 0) db_part[(int64_t)wave * ldg + n * 16 + i] = s;
+    }
+}
+
+// ---- B: dW partial slabs -----------------------------------------------------
+// Block blk reduces rows [blk*rows_per, ...) into slab[blk][C16][K].  Wave w
+// owns the K column groups {w, w+4, ...} of 16*V columns each.  MFMA k-step =
+// 4 rows: A[i=class][k=row] = G[row][class] (lane l: G[r0+(l>>4)][n*16+(l&15)]),
+// B[k=row][j] = X[r0+(l>>4)][c0 + (l&15)*V + v] for MFMA v.
+template <int V, int NT, int CT>
+__global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ X, int64_t ldx,
+                                                     const float *__restrict__ G, int ldg, int M,
+                                                     int K, int rows_per,
+                                                     float *__restrict__ slab) {
+    using VT = typename Vec<V>::T;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int r_begin = blockIdx.x * rows_per;
+    const int r_end = min(M, r_begin + rows_per);
+    const int group_cols = 16 * V;
+    const int n_groups = (K + group_cols - 1) / group_cols;
+    float *out = slab + (int64_t)blockIdx.x * (NT * 16) * K;
+    for (int gb = w; gb < n_groups; gb += 4 * CT) {
+        f32x4 acc[NT][CT][V];
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+                for (int v = 0; v < V; ++v) acc[n][ct][v] = f32x4{0.f, 0.f, 0.f, 0.f};
+        int coff[CT];
+        bool cok[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+            const int c = (gb + ct * 4) * group_cols + i * V;
+            cok[ct] = c < K;
+            coff[ct] = cok[ct] ? c : 0;
+        }
+        for (int r0 = r_begin; r0 < r_end; r0 += 4) {
+            const int r = r0 + g;
+            const bool rok = r < r_end;
+            const int rr = rok ? r : r_begin;
+            float ga[NT];
+#pragma unroll
+            for (int n = 0; n < NT; ++n) ga[n] = rok ? G[(int64_t)rr * ldg + n * 16 + i] : 0.f;
+            const float *xr = X + (int64_t)rr * ldx;
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                VT xb = *reinterpret_cast<const VT *>(xr + coff[ct]);
+                if (!rok || !cok[ct]) xb = VT{};
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+#pragma unroll
+                    for (int n = 0; n < NT; ++n)
+                        acc[n][ct][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            ga[n], lane_elem<V>(xb, v), acc[n][ct][v], 0, 0, 0);
+            }
+        }
+        // D[class = 4*(l>>4)+q][j = l&15] of MFMA (n, ct, v) -> column c(j) + v
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) {
+                const int c = (gb + ct * 4) * group_cols + i * V;
+                if (!cok[ct]) continue;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int cls = n * 16 + g * 4 + q;
+#pragma unroll
+                    for (int v = 0; v < V; ++v) out[(int64_t)cls * K + c + v] = acc[n][ct][v][q];
+                }
+            }
+    }
+}
+
+// ---- C: fixed-order reductions ----------------------------------------------
+__global__ void xent_reduce_dw_kernel(const float *__restrict__ slab, int n_slabs, int C, int K,
+                                      int C16, float *__restrict__ dW) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)C * K;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t cls = e / K, k = e - cls * K;
+        float s = 0.f;
+        for (int j = 0; j < n_slabs; ++j) s += slab[((int64_t)j * C16 + cls) * K + k];
+        dW[e] = s;
+    }
+}
+
+__global__ void xent_reduce_small_kernel(const double *__restrict__ loss_part,
+                                         const float *__restrict__ db_part, int n_waves, int C,
+                                         int ldg, double inv_m, float *__restrict__ loss,
+                                         float *__restrict__ db) {
+    const int t = threadIdx.x;
+    if (t < C && db) {
+        float s = 0.f;
+        for (int j = 0; j < n_waves; ++j) s += db_part[(int64_t)j * ldg + t];
+        db[t] = s;
+    }
+    if (t == 0) {
+        double s = 0.0;
+        for (int j = 0; j < n_waves; ++j) s += loss_part[j];
+        *loss = (float)(s * inv_m);
+    }
+}
+
+template <int V, int NT>
+hipError_t launch_fwd(const float *X, int64_t ldx, const float *W, const float *b,
+                      const int64_t *labels, int M, int K, int C, float *G, int ldg,
+                      double *loss_part, float *db_part, float *logits, int64_t ldl,
+                      hipStream_t s) {
+    constexpr int MT = 4;
+    const int waves = (M + MT * 16 - 1) / (MT * 16);
+    const int blocks = (waves + 3) / 4;
+    hipLaunchKernelGGL((xent_fwd_kernel<V, MT, NT>), dim3(blocks), dim3(256), 0, s, X, ldx, W, b,
+                       labels, M, K, C, 1.0f / (float)M, G, ldg, loss_part, db_part, logits, ldl);
+    return hipGetLastError();
+}
+
+template <int V, int NT>
+hipError_t launch_dw(const float *X, int64_t ldx, const float *G, int ldg, int M, int K,
+                     int n_slabs, int rows_per, float *slab, hipStream_t s) {
+    constexpr int CT = (NT >= 3) ? 2 : 4;
+    hipLaunchKernelGGL((xent_dw_kernel<V, NT, CT>), dim3(n_slabs), dim3(256), 0, s, X, ldx, G,
+                       ldg, M, K, rows_per, slab);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+int64_t xent_workspace_bytes(int64_t M, int64_t K, int64_t C) {
+    if (M <= 0 || K <= 0 || C <= 0) return 0;
+    const int64_t C16 = (C + 15) / 16 * 16;
+    const int64_t waves = (M + 63) / 64;
+    const int64_t n_slabs = std::min<int64_t>(512, (M + 255) / 256);
+    auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+    return al(M * C16 * 4) + al(waves * 8) + al(waves * C16 * 4) + al(n_slabs * C16 * K * 4) + 512;
+}
+
+int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
+                    const int64_t *labels, int64_t M, int64_t K, int64_t C, float *loss,
+                    float *dW, float *db, float *logits, int64_t ldl, void *ws, int64_t ws_bytes,
+                    hipStream_t s) {
+    SGC_REQUIRE(X && W && labels && loss && dW && ws, SGC_EINVAL, "linear_xent: null pointer");
+    SGC_REQUIRE(M > 0 && K > 0 && C > 0 && C <= 64 && ldx >= K, SGC_EINVAL,
+                "linear_xent: bad shape M=%lld K=%lld C=%lld (C <= 64)", (long long)M,
+                (long long)K, (long long)C);
+    SGC_REQUIRE(M < INT32_MAX && K < INT32_MAX, SGC_ERANGE, "linear_xent: too large");
+    SGC_REQUIRE(!logits || ldl >= C, SGC_EINVAL, "linear_xent: ldl < C");
+    const int64_t need = xent_workspace_bytes(M, K, C);
+    SGC_REQUIRE(ws_bytes >= need, SGC_ENOMEM, "linear_xent: workspace %lld < %lld",
+                (long long)ws_bytes, (long long)need);
+    const int NT = (int)((C + 15) / 16);
+    const int C16 = NT * 16;
+    const int waves = (int)((M + 63) / 64);
+    const int n_slabs = (int)std::min<int64_t>(512, (M + 255) / 256);
+    const int rows_per = (int)(((M + n_slabs - 1) / n_slabs + 3) / 4 * 4);
+    auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+    char *p = (char *)(((uintptr_t)ws + 255) & ~uintptr_t(255));
+    float *G = (float *)p;
+    p += al(M * C16 * 4);
+    double *loss_part = (double *)p;
+    p += al((int64_t)waves * 8);
+    float *db_part = (float *)p;
+    p += al((int64_t)waves * C16 * 4);
+    float *slab = (float *)p;
+
+    int V = 1;
+    for (int v : {4, 2})
+        if (K % v == 0 && ldx % v == 0 && (uintptr_t)X % (4 * v) == 0 && (uintptr_t)W % (4 * v) == 0) {
+            V = v;
+            break;
+        }
+    hipError_t e = hipSuccess;
+#define SGC_XENT_DISPATCH(VV)                                                                    \
+    switch (NT) {                                                                                \
+        case 1: e = launch_fwd<VV, 1>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,      \
+                                      loss_part, db_part, logits, ldl, s);                       \
+            if (e == hipSuccess) e = launch_dw<VV, 1>(X, ldx, G, C16, (int)M, (int)K, n_slabs,   \
+                                                      rows_per, slab, s);                        \
+            break;                                                                               \
+        case 2: e = launch_fwd<VV, 2>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,      \
+                                      loss_part, db_part, logits, ldl, s);                       \
+            if (e == hipSuccess) e = launch_dw<VV, 2>(X, ldx, G, C16, (int)M, (int)K, n_slabs,   \
+                                                      rows_per, slab, s);                        \
+            break;                                                                               \
+        case 3: e = launch_fwd<VV, 3>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,      \
+                                      loss_part, db_part, logits, ldl, s);                       \
+            if (e == hipSuccess) e = launch_dw<VV, 3>(X, ldx, G, C16, (int)M, (int)K, n_slabs,   \
+                                                      rows_per, slab, s);                        \
+            break;                                                                               \
+        default: e = launch_fwd<VV, 4>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,     \
+                                       loss_part, db_part, logits, ldl, s);                      \
+            if (e == hipSuccess) e = launch_dw<VV, 4>(X, ldx, G, C16, (int)M, (int)K, n_slabs,   \
+                                                      rows_per, slab, s);                        \
+            break;                                                                               \
+    }
+    if (V == 4) {
+        SGC_XENT_DISPATCH(4)
+    } else if (V == 2) {
+        SGC_XENT_DISPATCH(2)
+    } else {
+        SGC_XENT_DISPATCH(1)
+    }
+#undef SGC_XENT_DISPATCH
+    SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear_xent launch failed: %s", hipGetErrorString(e));
+    const int64_t ck = C * K;
+    const int rblocks = (int)std::min<int64_t>((ck + 255) / 256, 4096);
+    hipLaunchKernelGGL(xent_reduce_dw_kernel, dim3(rblocks), dim3(256), 0, s, slab, n_slabs,
+                       (int)C, (int)K, C16, dW);
+    SGC_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(xent_reduce_small_kernel, dim3(1), dim3(64), 0, s, loss_part, db_part,
+                       waves, (int)C, C16, 1.0 / (double)M, loss, db);
+    SGC_HIP_CHECK(hipGetLastError());
+    return SGC_OK;
+}
+
+}  // namespace sgc

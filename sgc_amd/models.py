@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 
 from .propagate import linear as _mfma_linear
+from .propagate import linear_xent as _fused_xent
 
 
 class _LinearMFMA(torch.autograd.Function):
@@ -27,6 +28,34 @@ class _LinearMFMA(torch.autograd.Function):
         gw = grad_out.t() @ x if ctx.needs_input_grad[1] else None
         gb = grad_out.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw, gb
+
+
+class _LinearCrossEntropy(torch.autograd.Function):
+    """loss = F.cross_entropy(x W^T + b, y) with dW, db from one fused pass
+    (sgc_linear_xent_f32); the gradients are computed in forward and scaled
+    by the incoming grad in backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, labels):
+        if ctx.needs_input_grad[0]:
+            raise NotImplementedError("fused SGC loss: no gradient w.r.t. the features")
+        loss, dW, db = _fused_xent(x, weight, bias, labels)
+        ctx.save_for_backward(dW, db if db is not None else dW.new_empty(0))
+        ctx.has_bias = bias is not None
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        dW, db = ctx.saved_tensors
+        return None, grad_loss * dW, (grad_loss * db if ctx.has_bias else None), None
+
+
+def sgc_cross_entropy(model, features, labels):
+    """F.cross_entropy(model(features), labels) for an SGC model, fused on the
+    GPU: one launch chain computes the loss and the W/b gradients (the
+    reference closure, citation.py:47-49 / reddit.py:55-58).  Works with Adam
+    and LBFGS exactly like the unfused expression."""
+    return _LinearCrossEntropy.apply(features, model.W.weight, model.W.bias, labels)
 
 
 class SGC(nn.Module):

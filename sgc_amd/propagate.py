@@ -294,3 +294,37 @@ def linear(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
                                       _lib.ptr(out), out.stride(0), M, K, C,
                                       _lib.stream_handle(X.device)), "linear_f32")
     return out
+
+
+def linear_xent(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                labels: torch.Tensor, want_logits=False):
+    """Fused SGC training step: (loss, dW, db[, logits]) for
+    F.cross_entropy(X W^T + b, labels) (mean), on the GPU (sgc_linear_xent_f32)."""
+    _require_device(X, "input")
+    if X.dtype != torch.float32 or weight.dtype != torch.float32:
+        raise TypeError("sgc_amd.linear_xent: float32 only")
+    M, K = X.shape
+    C = weight.shape[0]
+    if weight.shape[1] != K or labels.shape != (M,):
+        raise RuntimeError("sgc_amd.linear_xent: shape mismatch")
+    if C > 64:
+        raise ValueError("sgc_amd.linear_xent: at most 64 classes")
+    if X.stride(1) != 1 or X.stride(0) < K:
+        X = X.contiguous()
+    W = weight.detach().contiguous()
+    b = bias.detach().contiguous() if bias is not None else None
+    y = labels.to(device=X.device, dtype=torch.int64).contiguous()
+    lib = _lib.load()
+    loss = torch.empty((), dtype=torch.float32, device=X.device)
+    dW = torch.empty_like(W)
+    db = torch.empty(C, dtype=torch.float32, device=X.device) if b is not None else None
+    logits = torch.empty((M, C), dtype=torch.float32, device=X.device) if want_logits else None
+    ws_bytes = lib.sgc_linear_xent_workspace(M, K, C)
+    ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8, device=X.device)
+    with torch.cuda.device(X.device):
+        _lib.check(lib.sgc_linear_xent_f32(_lib.ptr(X), X.stride(0), _lib.ptr(W), _lib.ptr(b),
+                                           _lib.ptr(y), M, K, C, _lib.ptr(loss), _lib.ptr(dW),
+                                           _lib.ptr(db), _lib.ptr(logits), C, _lib.ptr(ws),
+                                           ws_bytes, _lib.stream_handle(X.device)),
+                   "linear_xent_f32")
+    return (loss, dW, db, logits) if want_logits else (loss, dW, db)

@@ -234,3 +234,53 @@ def test_sgc_model_autograd_matches_torch():
     torch.testing.assert_close(m.W.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(m.W.bias.grad, ref.bias.grad, rtol=1e-4, atol=1e-6)
     assert isinstance(get_model("SGC", 10, 3, cuda=True), SGC)
+
+
+@pytest.mark.parametrize("M,K,C", [(1, 3, 2), (140, 1433, 7), (333, 602, 41), (1000, 500, 3),
+                                   (4099, 602, 41), (77, 64, 64), (600, 130, 17)])
+def test_fused_xent_matches_torch(M, K, C):
+    """loss, dW, db of the fused training step vs fp64 torch (fp32 tolerance)."""
+    from sgc_amd.propagate import linear_xent
+    g = torch.Generator().manual_seed(M + K + C)
+    X = torch.randn((M, K), generator=g)
+    W = torch.randn((C, K), generator=g) * 0.05
+    b = torch.randn(C, generator=g) * 0.1
+    y = torch.randint(0, C, (M,), generator=g)
+    Wd, bd = W.double().requires_grad_(), b.double().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(torch.nn.functional.linear(X.double(), Wd, bd), y)
+    ref.backward()
+    loss, dW, db, logits = linear_xent(X.to(DEV), W.to(DEV), b.to(DEV), y.to(DEV), want_logits=True)
+    torch.testing.assert_close(loss.cpu().double(), ref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dW.cpu().double(), Wd.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(db.cpu().double(), bd.grad, rtol=1e-4, atol=1e-6)
+    zref = torch.nn.functional.linear(X.double(), W.double(), b.double())
+    torch.testing.assert_close(logits.cpu().double(), zref, rtol=1e-5,
+                               atol=1e-5 * max(1.0, zref.abs().max().item()))
+    # bitwise reproducible run to run (fixed-order reductions)
+    loss2, dW2, db2 = linear_xent(X.to(DEV), W.to(DEV), b.to(DEV), y.to(DEV))
+    assert torch.equal(loss, loss2) and torch.equal(dW, dW2) and torch.equal(db, db2)
+
+
+def test_fused_loss_trains_like_torch():
+    """LBFGS (reddit.py's optimiser) with the fused loss tracks the unfused path."""
+    from sgc_amd.models import SGC, sgc_cross_entropy
+    torch.manual_seed(0)
+    X = torch.randn(3000, 602, device=DEV)
+    y = torch.randint(0, 41, (3000,), device=DEV)
+    m1 = SGC(602, 41).to(DEV)
+    m2 = SGC(602, 41).to(DEV)
+    m2.load_state_dict(m1.state_dict())
+    losses = []
+    for m, fused in ((m1, True), (m2, False)):
+        opt = torch.optim.LBFGS(m.parameters(), lr=1)
+
+        def closure():
+            opt.zero_grad()
+            loss = sgc_cross_entropy(m, X, y) if fused else \
+                torch.nn.functional.cross_entropy(m(X), y)
+            loss.backward()
+            return loss
+        for _ in range(2):
+            opt.step(closure)
+        losses.append(torch.nn.functional.cross_entropy(m(X), y).item())
+    assert abs(losses[0] - losses[1]) <= 1e-3 * max(1.0, abs(losses[1])), losses
