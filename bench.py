@@ -136,7 +136,7 @@ def main():
     n, F, nnz = S.n, X_host.shape[1], S.nnz
     X0 = torch.from_numpy(X_host).to(dev)
 
-    n_launch = args.steps * K * (1 if world == 1 else -(-F // max(2, args.group_floats)))
+    n_launch = args.steps * K * (1 if world == 1 else -(-(F + 31) // 32 * 32 // max(2, args.group_floats)))
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(n_launch)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(n_launch)]
     launch_bytes = []
@@ -164,12 +164,12 @@ def main():
         shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
         from sgc_amd.distributed import _default_spmm
 
-        nnz_l = int(shard.row_ptr[-1].item())
+        nnz_l = shard.nnz
 
-        def timed_spmm(sh, col, X, out):
+        def timed_spmm(sh, X, out):
             if ev["on"]:
                 starts[ev["i"]].record()
-            r = _default_spmm(sh, col, X, out)
+            r = _default_spmm(sh, X, out)
             if ev["on"]:
                 ends[ev["i"]].record()
                 ev["i"] += 1

@@ -15,7 +15,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from sgc_amd.distributed import RowPartitionedPropagator, make_shard, nnz_balanced_bounds
+from sgc_amd.distributed import (RowPartitionedPropagator, equal_row_bounds, make_shard,
+                                 nnz_balanced_bounds)
 
 
 def _free_port():
@@ -35,10 +36,16 @@ def test_bounds_balance_nnz():
     assert b[0] == 0 and b[-1] == 2 and np.all(np.diff(b) >= 0)
 
 
-def _oracle_spmm(shard, col, X, out):
+def test_equal_row_bounds():
+    assert equal_row_bounds(10, 4).tolist() == [0, 3, 6, 9, 10]
+    assert equal_row_bounds(2, 4).tolist() == [0, 1, 2, 2, 2]
+    assert equal_row_bounds(8, 2).tolist() == [0, 4, 8]
+
+
+def _oracle_spmm(shard, X, out):
     from oracle import oracle as o
     rp = shard.row_ptr.numpy()
-    Y = o.spmm_csr(rp, col.numpy(), shard.val.numpy(), X.numpy())
+    Y = o.spmm_csr(rp, shard.col_idx.numpy(), shard.val.numpy(), X.numpy())
     out.copy_(torch.from_numpy(Y))
     return out
 
