@@ -182,7 +182,7 @@ def main():
 
         def step():
             return prop.propagate(X0, K, out=out_full)
-        parallelism = (f"row-partition x{world} (nnz-balanced) + per-hop all-gather "
+        parallelism = (f"row-partition x{world} (equal-row blocks) + per-hop all-gather "
                        f"({'rccl' if args.dist_backend == 'nccl' else 'gloo rehearsal'}), "
                        f"pipelined in {args.group_floats}-float feature groups")
 

@@ -9,13 +9,12 @@
 // so one step covers 4V values of k with V MFMAs; MFMA v sums k = k0+g*V+v
 // over the lane groups g = 0..3.  A wave owns MT x 16 rows and all classes
 // (NT x 16, padded), so X is read exactly once from HBM; W (nclass x nfeat,
-// 99 KB at Reddit shape) is re-read per wave from L2.  The kernel is
-// HBM-bound on X at the Reddit shape (0.5 flop/B).
-#include "common.h"
+// 99 KB at Reddit shape) is re-read per wave from L2.  At the Reddit-train
+// shape the fp32 MFMA work (2 x 152,410 x 602 x 48 = 8.8 GFLOP, 56 us at
+// 157 TF) and the X read (367 MB, ~60 us) are about even.
+#include "gemm_tile.h"
 
 namespace sgc {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int V, int MT, int NT>
 __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ X, int64_t ldx,
@@ -23,7 +22,6 @@ __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ X
                                                      const float *__restrict__ b,
                                                      float *__restrict__ Y, int64_t ldy, int M,
                                                      int K, int C) {
-    using VT = typename Vec<V>::T;
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     const int m0 = wave * (MT * 16);
@@ -43,35 +41,7 @@ __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ X
         wrow[n] = W + (int64_t)c * K;
     }
     f32x4 acc[MT][NT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-        for (int n = 0; n < NT; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    for (int k0 = 0; k0 < K; k0 += 4 * V) {
-        const int k = k0 + g * V;
-        const bool ok = k < K;
-        const int kk = ok ? k : 0;
-        VT xa[MT], wb[NT];
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-            xa[t] = *reinterpret_cast<const VT *>(xrow[t] + kk);
-            if (!ok) xa[t] = VT{};
-        }
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-            wb[n] = *reinterpret_cast<const VT *>(wrow[n] + kk);
-            if (!ok) wb[n] = VT{};
-        }
-#pragma unroll
-        for (int v = 0; v < V; ++v)
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-                    acc[t][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                        lane_elem<V>(xa[t], v), lane_elem<V>(wb[n], v), acc[t][n], 0, 0, 0);
-    }
+    xwt_tile<V, MT, NT>(xrow, wrow, K, g, acc);
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
         const int c = n * 16 + i;
@@ -104,9 +74,9 @@ template <int V>
 hipError_t dispatch_nt(int nt, const float *X, int64_t ldx, const float *W, const float *b,
                        float *Y, int64_t ldy, int M, int K, int C, hipStream_t s) {
     switch (nt) {
-        case 1: return launch_linear<V, 4, 1>(X, ldx, W, b, Y, ldy, M, K, C, s);
-        case 2: return launch_linear<V, 4, 2>(X, ldx, W, b, Y, ldy, M, K, C, s);
-        case 3: return launch_linear<V, 4, 3>(X, ldx, W, b, Y, ldy, M, K, C, s);
+        case 1: return launch_linear<V, 2, 1>(X, ldx, W, b, Y, ldy, M, K, C, s);
+        case 2: return launch_linear<V, 2, 2>(X, ldx, W, b, Y, ldy, M, K, C, s);
+        case 3: return launch_linear<V, 2, 3>(X, ldx, W, b, Y, ldy, M, K, C, s);
         case 4: return launch_linear<V, 2, 4>(X, ldx, W, b, Y, ldy, M, K, C, s);
         default: return hipErrorInvalidValue;
     }

@@ -16,11 +16,11 @@
 //                         B = X rows, V-vector loads split over V MFMAs);
 //   C  xent_reduce_kernel slabs -> dW, per-wave partials -> db and loss, in a
 //                         fixed order (bitwise reproducible run to run).
-#include "common.h"
+#include "gemm_tile.h"
 
 namespace sgc {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kXentMT = 2;  // 32 rows of X per wave in the forward kernel
 
 namespace {
 
@@ -42,7 +42,6 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(
     const float *__restrict__ b, const int64_t *__restrict__ labels, int M, int K, int C,
     float inv_m, float *__restrict__ G, int ldg, double *__restrict__ loss_part,
     float *__restrict__ db_part, float *__restrict__ logits, int64_t ldl) {
-    using VT = typename Vec<V>::T;
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
     const int m0 = wave * (MT * 16);
@@ -60,34 +59,7 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(
 #pragma unroll
         for (int n = 0; n < NT; ++n) wrow[n] = W + (int64_t)min(n * 16 + i, C - 1) * K;
         f32x4 acc[MT][NT];
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-#pragma unroll
-            for (int n = 0; n < NT; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int k0 = 0; k0 < K; k0 += 4 * V) {
-            const int k = k0 + g * V;
-            const bool ok = k < K;
-            const int kk = ok ? k : 0;
-            VT xa[MT], wb[NT];
-#pragma unroll
-            for (int t = 0; t < MT; ++t) {
-                xa[t] = *reinterpret_cast<const VT *>(xrow[t] + kk);
-                if (!ok) xa[t] = VT{};
-            }
-#pragma unroll
-            for (int n = 0; n < NT; ++n) {
-                wb[n] = *reinterpret_cast<const VT *>(wrow[n] + kk);
-                if (!ok) wb[n] = VT{};
-            }
-#pragma unroll
-            for (int v = 0; v < V; ++v)
-#pragma unroll
-                for (int t = 0; t < MT; ++t)
-#pragma unroll
-                    for (int n = 0; n < NT; ++n)
-                        acc[t][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                            lane_elem<V>(xa[t], v), lane_elem<V>(wb[n], v), acc[t][n], 0, 0, 0);
-        }
+        xwt_tile<V, MT, NT>(xrow, wrow, K, g, acc);
         float bias[NT];
         bool valid[NT];
 #pragma unroll
@@ -183,25 +155,36 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
             cok[ct] = c < K;
             coff[ct] = cok[ct] ? c : 0;
         }
-        for (int r0 = r_begin; r0 < r_end; r0 += 4) {
+        float ga[NT], gn[NT];
+        VT xb[CT], xn[CT];
+        auto load = [&](int r0, float (&gd)[NT], VT (&xd)[CT]) {
             const int r = r0 + g;
             const bool rok = r < r_end;
             const int rr = rok ? r : r_begin;
-            float ga[NT];
 #pragma unroll
-            for (int n = 0; n < NT; ++n) ga[n] = rok ? G[(int64_t)rr * ldg + n * 16 + i] : 0.f;
+            for (int n = 0; n < NT; ++n) gd[n] = rok ? G[(int64_t)rr * ldg + n * 16 + i] : 0.f;
             const float *xr = X + (int64_t)rr * ldx;
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) {
-                VT xb = *reinterpret_cast<const VT *>(xr + coff[ct]);
-                if (!rok || !cok[ct]) xb = VT{};
+                xd[ct] = *reinterpret_cast<const VT *>(xr + coff[ct]);
+                if (!rok || !cok[ct]) xd[ct] = VT{};
+            }
+        };
+        if (r_begin < r_end) load(r_begin, ga, xb);
+        for (int r0 = r_begin; r0 < r_end; r0 += 4) {
+            if (r0 + 4 < r_end) load(r0 + 4, gn, xn);
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
                 for (int v = 0; v < V; ++v)
 #pragma unroll
                     for (int n = 0; n < NT; ++n)
                         acc[n][ct][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                            ga[n], lane_elem<V>(xb, v), acc[n][ct][v], 0, 0, 0);
-            }
+                            ga[n], lane_elem<V>(xb[ct], v), acc[n][ct][v], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n) ga[n] = gn[n];
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) xb[ct] = xn[ct];
         }
         // D[class = 4*(l>>4)+q][j = l&15] of MFMA (n, ct, v) -> column c(j) + v
 #pragma unroll
@@ -221,31 +204,65 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
 }
 
 // ---- C: fixed-order reductions ----------------------------------------------
-__global__ void xent_reduce_dw_kernel(const float *__restrict__ slab, int n_slabs, int C, int K,
-                                      int C16, float *__restrict__ dW) {
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < (int64_t)C * K;
-         e += (int64_t)gridDim.x * blockDim.x) {
+// dW: a block owns 64 consecutive elements; wave w sums slabs [w*n/4, (w+1)*n/4)
+// in order (coalesced 256-B rows of each slab), then wave 0 adds the four
+// partials in order.  Deterministic; ~n/4 loads in flight per lane.
+__global__ __launch_bounds__(256) void xent_reduce_dw_kernel(const float *__restrict__ slab,
+                                                             int n_slabs, int C, int K, int C16,
+                                                             float *__restrict__ dW) {
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t e = blockIdx.x * 64LL + lane;
+    const int64_t total = (int64_t)C * K;
+    const int j0 = (int)((int64_t)n_slabs * w / 4), j1 = (int)((int64_t)n_slabs * (w + 1) / 4);
+    float s = 0.f;
+    if (e < total) {
         const int64_t cls = e / K, k = e - cls * K;
-        float s = 0.f;
-        for (int j = 0; j < n_slabs; ++j) s += slab[((int64_t)j * C16 + cls) * K + k];
-        dW[e] = s;
+        const float *p = slab + cls * K + k;
+        const int64_t stride = (int64_t)C16 * K;
+        int j = j0;
+        for (; j + 8 <= j1; j += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(j + u) * stride];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; j < j1; ++j) s += p[(int64_t)j * stride];
     }
+    part[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && e < total) dW[e] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
-__global__ void xent_reduce_small_kernel(const double *__restrict__ loss_part,
-                                         const float *__restrict__ db_part, int n_waves, int C,
-                                         int ldg, double inv_m, float *__restrict__ loss,
-                                         float *__restrict__ db) {
+// loss (double) and db: one block, 256 threads, strided partial sums then a
+// fixed-shape LDS tree -- deterministic.
+__global__ __launch_bounds__(256) void xent_reduce_small_kernel(
+    const double *__restrict__ loss_part, const float *__restrict__ db_part, int n_waves, int C,
+    int ldg, double inv_m, float *__restrict__ loss, float *__restrict__ db) {
+    __shared__ double red[256];
     const int t = threadIdx.x;
-    if (t < C && db) {
-        float s = 0.f;
-        for (int j = 0; j < n_waves; ++j) s += db_part[(int64_t)j * ldg + t];
-        db[t] = s;
+    double s = 0.0;
+    for (int j = t; j < n_waves; j += 256) s += loss_part[j];
+    red[t] = s;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (t < h) red[t] += red[t + h];
+        __syncthreads();
     }
-    if (t == 0) {
-        double s = 0.0;
-        for (int j = 0; j < n_waves; ++j) s += loss_part[j];
-        *loss = (float)(s * inv_m);
+    if (t == 0) *loss = (float)(red[0] * inv_m);
+    if (!db) return;
+    for (int c = 0; c < C; ++c) {
+        __syncthreads();
+        float f = 0.f;
+        for (int j = t; j < n_waves; j += 256) f += db_part[(int64_t)j * ldg + c];
+        red[t] = (double)f;
+        __syncthreads();
+        for (int h = 128; h > 0; h >>= 1) {
+            if (t < h) red[t] += red[t + h];
+            __syncthreads();
+        }
+        if (t == 0) db[c] = (float)red[0];
     }
 }
 
@@ -254,7 +271,7 @@ hipError_t launch_fwd(const float *X, int64_t ldx, const float *W, const float *
                       const int64_t *labels, int M, int K, int C, float *G, int ldg,
                       double *loss_part, float *db_part, float *logits, int64_t ldl,
                       hipStream_t s) {
-    constexpr int MT = 4;
+    constexpr int MT = kXentMT;
     const int waves = (M + MT * 16 - 1) / (MT * 16);
     const int blocks = (waves + 3) / 4;
     hipLaunchKernelGGL((xent_fwd_kernel<V, MT, NT>), dim3(blocks), dim3(256), 0, s, X, ldx, W, b,
@@ -276,7 +293,7 @@ hipError_t launch_dw(const float *X, int64_t ldx, const float *G, int ldg, int M
 int64_t xent_workspace_bytes(int64_t M, int64_t K, int64_t C) {
     if (M <= 0 || K <= 0 || C <= 0) return 0;
     const int64_t C16 = (C + 15) / 16 * 16;
-    const int64_t waves = (M + 63) / 64;
+    const int64_t waves = (M + 16 * kXentMT - 1) / (16 * kXentMT);
     const int64_t n_slabs = std::min<int64_t>(512, (M + 255) / 256);
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     return al(M * C16 * 4) + al(waves * 8) + al(waves * C16 * 4) + al(n_slabs * C16 * K * 4) + 512;
@@ -297,7 +314,7 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
                 (long long)ws_bytes, (long long)need);
     const int NT = (int)((C + 15) / 16);
     const int C16 = NT * 16;
-    const int waves = (int)((M + 63) / 64);
+    const int waves = (int)((M + 16 * kXentMT - 1) / (16 * kXentMT));
     const int n_slabs = (int)std::min<int64_t>(512, (M + 255) / 256);
     const int rows_per = (int)(((M + n_slabs - 1) / n_slabs + 3) / 4 * 4);
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
@@ -350,11 +367,10 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
 #undef SGC_XENT_DISPATCH
     SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear_xent launch failed: %s", hipGetErrorString(e));
     const int64_t ck = C * K;
-    const int rblocks = (int)std::min<int64_t>((ck + 255) / 256, 4096);
-    hipLaunchKernelGGL(xent_reduce_dw_kernel, dim3(rblocks), dim3(256), 0, s, slab, n_slabs,
-                       (int)C, (int)K, C16, dW);
+    hipLaunchKernelGGL(xent_reduce_dw_kernel, dim3((unsigned)((ck + 63) / 64)), dim3(256), 0, s,
+                       slab, n_slabs, (int)C, (int)K, C16, dW);
     SGC_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(xent_reduce_small_kernel, dim3(1), dim3(64), 0, s, loss_part, db_part,
+    hipLaunchKernelGGL(xent_reduce_small_kernel, dim3(1), dim3(256), 0, s, loss_part, db_part,
                        waves, (int)C, C16, 1.0 / (double)M, loss, db);
     SGC_HIP_CHECK(hipGetLastError());
     return SGC_OK;
