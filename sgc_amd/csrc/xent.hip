@@ -235,34 +235,33 @@ __global__ __launch_bounds__(256) void xent_reduce_dw_kernel(const float *__rest
     if (w == 0 && e < total) dW[e] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
-// loss (double) and db: one block, 256 threads, strided partial sums then a
-// fixed-shape LDS tree -- deterministic.
+// loss (double, block C) and db (block c < C): 256 threads per block, strided
+// partial sums then a fixed-shape LDS tree -- deterministic.
 __global__ __launch_bounds__(256) void xent_reduce_small_kernel(
     const double *__restrict__ loss_part, const float *__restrict__ db_part, int n_waves, int C,
     int ldg, double inv_m, float *__restrict__ loss, float *__restrict__ db) {
     __shared__ double red[256];
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, c = blockIdx.x;
+    if (c < C && !db) return;
     double s = 0.0;
-    for (int j = t; j < n_waves; j += 256) s += loss_part[j];
+    if (c == C) {
+        for (int j = t; j < n_waves; j += 256) s += loss_part[j];
+    } else {
+        float f = 0.f;
+        for (int j = t; j < n_waves; j += 256) f += db_part[(int64_t)j * ldg + c];
+        s = f;
+    }
     red[t] = s;
     __syncthreads();
     for (int h = 128; h > 0; h >>= 1) {
         if (t < h) red[t] += red[t + h];
         __syncthreads();
     }
-    if (t == 0) *loss = (float)(red[0] * inv_m);
-    if (!db) return;
-    for (int c = 0; c < C; ++c) {
-        __syncthreads();
-        float f = 0.f;
-        for (int j = t; j < n_waves; j += 256) f += db_part[(int64_t)j * ldg + c];
-        red[t] = (double)f;
-        __syncthreads();
-        for (int h = 128; h > 0; h >>= 1) {
-            if (t < h) red[t] += red[t + h];
-            __syncthreads();
-        }
-        if (t == 0) db[c] = (float)red[0];
+    if (t == 0) {
+        if (c == C)
+            *loss = (float)(red[0] * inv_m);
+        else
+            db[c] = (float)red[0];
     }
 }
 
@@ -370,7 +369,7 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
     hipLaunchKernelGGL(xent_reduce_dw_kernel, dim3((unsigned)((ck + 63) / 64)), dim3(256), 0, s,
                        slab, n_slabs, (int)C, (int)K, C16, dW);
     SGC_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(xent_reduce_small_kernel, dim3(1), dim3(256), 0, s, loss_part, db_part,
+    hipLaunchKernelGGL(xent_reduce_small_kernel, dim3((unsigned)C + 1), dim3(256), 0, s, loss_part, db_part,
                        waves, (int)C, C16, 1.0 / (double)M, loss, db);
     SGC_HIP_CHECK(hipGetLastError());
     return SGC_OK;
