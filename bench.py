@@ -38,6 +38,8 @@ from sgc_amd import graphs  # noqa: E402
 from sgc_amd.propagate import DeviceCSR, propagate  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BASELINE_METRIC = ("propagated edges/sec (K-hop SpMM) + precompute wall-time, "
+                   "Reddit K=2 at 1/2/4/8 GPUs")
 
 
 def algorithmic_bytes_per_hop(n, nnz, F):
@@ -224,7 +226,8 @@ def main():
     rec = None
     if rank == 0:
         rec = {
-            "metric": "propagated edges/sec (K-hop SpMM), Reddit-shape K=2",
+            "metric": (BASELINE_METRIC if args.shape == "reddit" and K == 2 else
+                       f"propagated edges/sec (K-hop SpMM), {args.shape}-shape K={K}"),
             "value": value,
             "unit": "edges/s",
             "n_gpus": world,
