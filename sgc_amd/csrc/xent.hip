@@ -155,24 +155,19 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
             cok[ct] = c < K;
             coff[ct] = cok[ct] ? c : 0;
         }
+        // Columns past K read column 0 (finite) and are never stored; rows past
+        // r_end only occur in the ragged last step, which zeroes their G.
         float ga[NT], gn[NT];
         VT xb[CT], xn[CT];
         auto load = [&](int r0, float (&gd)[NT], VT (&xd)[CT]) {
-            const int r = r0 + g;
-            const bool rok = r < r_end;
-            const int rr = rok ? r : r_begin;
+            const int64_t r = r0 + g;
 #pragma unroll
-            for (int n = 0; n < NT; ++n) gd[n] = rok ? G[(int64_t)rr * ldg + n * 16 + i] : 0.f;
-            const float *xr = X + (int64_t)rr * ldx;
+            for (int n = 0; n < NT; ++n) gd[n] = G[r * ldg + n * 16 + i];
+            const float *xr = X + r * ldx;
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) {
-                xd[ct] = *reinterpret_cast<const VT *>(xr + coff[ct]);
-                if (!rok || !cok[ct]) xd[ct] = VT{};
-            }
+            for (int ct = 0; ct < CT; ++ct) xd[ct] = *reinterpret_cast<const VT *>(xr + coff[ct]);
         };
-        if (r_begin < r_end) load(r_begin, ga, xb);
-        for (int r0 = r_begin; r0 < r_end; r0 += 4) {
-            if (r0 + 4 < r_end) load(r0 + 4, gn, xn);
+        auto mma = [&](const float (&gd)[NT], const VT (&xd)[CT]) {
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
@@ -180,11 +175,32 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
 #pragma unroll
                     for (int n = 0; n < NT; ++n)
                         acc[n][ct][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                            ga[n], lane_elem<V>(xb[ct], v), acc[n][ct][v], 0, 0, 0);
+                            gd[n], lane_elem<V>(xd[ct], v), acc[n][ct][v], 0, 0, 0);
+        };
+        const int n_full = (r_end - r_begin) / 4;
+        const int r_main = r_begin + 4 * n_full;
+        int r0 = r_begin;
+        if (n_full > 0) load(r0, ga, xb);
+        for (; r0 + 8 <= r_main; r0 += 8) {
+            load(r0 + 4, gn, xn);
+            mma(ga, xb);
+            if (r0 + 8 < r_main) load(r0 + 8, ga, xb);
+            mma(gn, xn);
+        }
+        if (r0 < r_main) {
+            mma(ga, xb);
+            r0 += 4;
+        }
+        if (r0 < r_end) {  // ragged tail: rows past r_end get G = 0
+            const int r = r0 + g;
+            const bool rok = r < r_end;
+            const int64_t rr = rok ? r : r_begin;
 #pragma unroll
-            for (int n = 0; n < NT; ++n) ga[n] = gn[n];
+            for (int n = 0; n < NT; ++n) ga[n] = rok ? G[rr * ldg + n * 16 + i] : 0.f;
+            const float *xr = X + rr * ldx;
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) xb[ct] = xn[ct];
+            for (int ct = 0; ct < CT; ++ct) xb[ct] = *reinterpret_cast<const VT *>(xr + coff[ct]);
+            mma(ga, xb);
         }
         // D[class = 4*(l>>4)+q][j = l&15] of MFMA (n, ct, v) -> column c(j) + v
 #pragma unroll
