@@ -75,3 +75,100 @@ __device__ __forceinline__ void xwt_tile(const float *const (&xrow)[MT],
 }
 
 }  // namespace sgc
+
+namespace sgc {
+
+// LDS-staged block tile for the classifier GEMMs: a 256-thread block owns
+// kLdsBM = 128 rows of X and every class (NT x 16); wave w computes rows
+// [32w, 32w + 32) (MT = 2) from LDS.  Per K-chunk of 32 the block stages X
+// [128 x 32] (16 consecutive threads read one row's 128 B: coalesced) and W
+// [16NT x 32] through registers into LDS; the next chunk's global loads are in
+// flight while the current chunk's MFMAs run.  Compared with every wave
+// streaming its own W rows (xwt_tile), W leaves L2 once per block, not once
+// per wave, and X arrives in whole 128-B lines.
+constexpr int kLdsBM = 128;
+constexpr int kLdsBK = 32;
+constexpr int kLdsPad = kLdsBK + 1;  // row stride in LDS: conflict-free ds_read_b32 columns
+
+template <int V, int NT>
+struct LdsTile {
+    float xs[kLdsBM][kLdsPad];
+    float ws[NT * 16][kLdsPad];
+};
+
+template <int V, int NT>
+__device__ __forceinline__ void xwt_block_tile(const float *__restrict__ X, int64_t ldx,
+                                               const float *__restrict__ W, int M, int K, int C,
+                                               int m_blk, LdsTile<V, NT> &sm,
+                                               f32x4 (&acc)[2][NT]) {
+    using VT = typename Vec<V>::T;
+    constexpr int PER_ROW = kLdsBK / V;                      // vectors per row per chunk
+    constexpr int XV = kLdsBM * PER_ROW / 256;               // X vectors per thread
+    constexpr int WV = (NT * 16 * PER_ROW + 255) / 256;      // W vectors per thread
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int i = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    VT xr[XV], wr[WV];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int j = 0; j < XV; ++j) {
+            const int q = tid + 256 * j;
+            const int row = q / PER_ROW, k = k0 + (q % PER_ROW) * V;
+            const int m = m_blk + row;
+            const bool ok = m < M && k < K;
+            xr[j] = *reinterpret_cast<const VT *>(X + (int64_t)(ok ? m : 0) * ldx + (ok ? k : 0));
+            if (!ok) xr[j] = VT{};
+        }
+#pragma unroll
+        for (int j = 0; j < WV; ++j) {
+            const int q = tid + 256 * j;
+            const int c = q / PER_ROW, k = k0 + (q % PER_ROW) * V;
+            const bool ok = q < NT * 16 * PER_ROW && c < C && k < K;
+            wr[j] = *reinterpret_cast<const VT *>(W + (int64_t)(ok ? c : 0) * K + (ok ? k : 0));
+            if (!ok) wr[j] = VT{};
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int j = 0; j < XV; ++j) {
+            const int q = tid + 256 * j;
+            const int row = q / PER_ROW, kc = (q % PER_ROW) * V;
+#pragma unroll
+            for (int v = 0; v < V; ++v) sm.xs[row][kc + v] = lane_elem<V>(xr[j], v);
+        }
+#pragma unroll
+        for (int j = 0; j < WV; ++j) {
+            const int q = tid + 256 * j;
+            if (q < NT * 16 * PER_ROW) {
+                const int c = q / PER_ROW, kc = (q % PER_ROW) * V;
+#pragma unroll
+                for (int v = 0; v < V; ++v) sm.ws[c][kc + v] = lane_elem<V>(wr[j], v);
+            }
+        }
+    };
+    load(0);
+    for (int k0 = 0; k0 < K; k0 += kLdsBK) {
+        __syncthreads();  // the previous chunk's reads of LDS are done
+        store();
+        __syncthreads();
+        if (k0 + kLdsBK < K) load(k0 + kLdsBK);  // in flight during this chunk's MFMAs
+#pragma unroll
+        for (int kk = 0; kk < kLdsBK; kk += 4) {
+            float a[2], b[NT];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) a[t] = sm.xs[w * 32 + t * 16 + i][kk + g];
+#pragma unroll
+            for (int n = 0; n < NT; ++n) b[n] = sm.ws[n * 16 + i][kk + g];
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    acc[t][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[n], acc[t][n], 0, 0, 0);
+        }
+    }
+}
+
+}  // namespace sgc

@@ -5,50 +5,35 @@
 // cdna_hip_programming.md 3) -- lane l holds A[l&15][l>>4], B[l>>4][l&15],
 // D[4*(l>>4)+r][l&15].  A = 16 rows of X, B = 16 classes of W^T.
 //
-// Each lane loads V consecutive k of one X row (and of one W row) per step,
-// so one step covers 4V values of k with V MFMAs; MFMA v sums k = k0+g*V+v
-// over the lane groups g = 0..3.  A wave owns MT x 16 rows and all classes
-// (NT x 16, padded), so X is read exactly once from HBM; W (nclass x nfeat,
-// 99 KB at Reddit shape) is re-read per wave from L2.  At the Reddit-train
+// A 256-thread block owns 128 rows and all classes (NT x 16, padded); X and
+// W chunks are staged through LDS (gemm_tile.h: xwt_block_tile), so X is read
+// once from HBM in whole lines and W once per block from L2.  At the Reddit-train
 // shape the fp32 MFMA work (2 x 152,410 x 602 x 48 = 8.8 GFLOP, 56 us at
 // 157 TF) and the X read (367 MB, ~60 us) are about even.
 #include "gemm_tile.h"
 
 namespace sgc {
 
-template <int V, int MT, int NT>
+template <int V, int NT>
 __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ X, int64_t ldx,
                                                      const float *__restrict__ W,
                                                      const float *__restrict__ b,
                                                      float *__restrict__ Y, int64_t ldy, int M,
                                                      int K, int C) {
-    const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    const int m0 = wave * (MT * 16);
-    if (m0 >= M) return;
+    __shared__ LdsTile<V, NT> sm;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = lane & 15, g = lane >> 4;
-
-    const float *xrow[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-        const int m = min(m0 + t * 16 + i, M - 1);
-        xrow[t] = X + (int64_t)m * ldx;
-    }
-    const float *wrow[NT];
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-        const int c = min(n * 16 + i, C - 1);
-        wrow[n] = W + (int64_t)c * K;
-    }
-    f32x4 acc[MT][NT];
-    xwt_tile<V, MT, NT>(xrow, wrow, K, g, acc);
+    const int m_blk = blockIdx.x * kLdsBM;
+    f32x4 acc[2][NT];
+    xwt_block_tile<V, NT>(X, ldx, W, M, K, C, m_blk, sm, acc);
+    const int m0 = m_blk + w * 32;
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
         const int c = n * 16 + i;
         if (c >= C) continue;
         const float bias = b ? b[c] : 0.0f;
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int m = m0 + t * 16 + g * 4 + r;
@@ -59,14 +44,12 @@ __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ X
 
 namespace {
 
-template <int V, int MT, int NT>
+template <int V, int NT>
 hipError_t launch_linear(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                          int64_t ldy, int M, int K, int C, hipStream_t s) {
-    const int rows_per_wave = MT * 16;
-    const int64_t waves = (M + rows_per_wave - 1) / rows_per_wave;
-    const int64_t blocks = (waves + 3) / 4;
-    hipLaunchKernelGGL((linear_kernel<V, MT, NT>), dim3((unsigned)blocks), dim3(256), 0, s, X, ldx,
-                       W, b, Y, ldy, M, K, C);
+    const int64_t blocks = (M + kLdsBM - 1) / kLdsBM;
+    hipLaunchKernelGGL((linear_kernel<V, NT>), dim3((unsigned)blocks), dim3(256), 0, s, X, ldx, W,
+                       b, Y, ldy, M, K, C);
     return hipGetLastError();
 }
 
@@ -74,10 +57,10 @@ template <int V>
 hipError_t dispatch_nt(int nt, const float *X, int64_t ldx, const float *W, const float *b,
                        float *Y, int64_t ldy, int M, int K, int C, hipStream_t s) {
     switch (nt) {
-        case 1: return launch_linear<V, 2, 1>(X, ldx, W, b, Y, ldy, M, K, C, s);
-        case 2: return launch_linear<V, 2, 2>(X, ldx, W, b, Y, ldy, M, K, C, s);
-        case 3: return launch_linear<V, 2, 3>(X, ldx, W, b, Y, ldy, M, K, C, s);
-        case 4: return launch_linear<V, 2, 4>(X, ldx, W, b, Y, ldy, M, K, C, s);
+        case 1: return launch_linear<V, 1>(X, ldx, W, b, Y, ldy, M, K, C, s);
+        case 2: return launch_linear<V, 2>(X, ldx, W, b, Y, ldy, M, K, C, s);
+        case 3: return launch_linear<V, 3>(X, ldx, W, b, Y, ldy, M, K, C, s);
+        case 4: return launch_linear<V, 4>(X, ldx, W, b, Y, ldy, M, K, C, s);
         default: return hipErrorInvalidValue;
     }
 }

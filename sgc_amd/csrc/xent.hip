@@ -20,7 +20,6 @@
 
 namespace sgc {
 
-constexpr int kXentMT = 2;  // 32 rows of X per wave in the forward kernel
 
 namespace {
 
@@ -36,30 +35,25 @@ __device__ __forceinline__ float group16_sum(float v) {
 }
 
 // ---- A: logits -> G, loss / dG partials ------------------------------------
-template <int V, int MT, int NT>
+template <int V, int NT>
 __global__ __launch_bounds__(256) void xent_fwd_kernel(
     const float *__restrict__ X, int64_t ldx, const float *__restrict__ W,
     const float *__restrict__ b, const int64_t *__restrict__ labels, int M, int K, int C,
     float inv_m, float *__restrict__ G, int ldg, double *__restrict__ loss_part,
     float *__restrict__ db_part, float *__restrict__ logits, int64_t ldl) {
-    const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-    const int m0 = wave * (MT * 16);
-    if (m0 >= M) return;  // the partial arrays hold exactly ceil(M / 16MT) waves
+    __shared__ LdsTile<V, NT> sm;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wave = blockIdx.x * 4 + w;
     const int i = lane & 15, g = lane >> 4;
+    const int m_blk = blockIdx.x * kLdsBM;
+    const int m0 = m_blk + w * 32;
     double wave_loss = 0.0;
     float dbc[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) dbc[n] = 0.f;
     {
-        const float *xrow[MT];
-#pragma unroll
-        for (int t = 0; t < MT; ++t) xrow[t] = X + (int64_t)min(m0 + t * 16 + i, M - 1) * ldx;
-        const float *wrow[NT];
-#pragma unroll
-        for (int n = 0; n < NT; ++n) wrow[n] = W + (int64_t)min(n * 16 + i, C - 1) * K;
-        f32x4 acc[MT][NT];
-        xwt_tile<V, MT, NT>(xrow, wrow, K, g, acc);
+        f32x4 acc[2][NT];
+        xwt_block_tile<V, NT>(X, ldx, W, M, K, C, m_blk, sm, acc);
         float bias[NT];
         bool valid[NT];
 #pragma unroll
@@ -69,11 +63,11 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(
             bias[n] = (valid[n] && b) ? b[c] : 0.f;
         }
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int m = m0 + t * 16 + g * 4 + r;
-                const bool row_ok = m < M;  // wave-group uniform per (t, r, g)
+                const bool row_ok = m < M;  // uniform per (t, r, lane group)
                 float z[NT];
                 float mx = -INFINITY;
 #pragma unroll
@@ -286,10 +280,8 @@ hipError_t launch_fwd(const float *X, int64_t ldx, const float *W, const float *
                       const int64_t *labels, int M, int K, int C, float *G, int ldg,
                       double *loss_part, float *db_part, float *logits, int64_t ldl,
                       hipStream_t s) {
-    constexpr int MT = kXentMT;
-    const int waves = (M + MT * 16 - 1) / (MT * 16);
-    const int blocks = (waves + 3) / 4;
-    hipLaunchKernelGGL((xent_fwd_kernel<V, MT, NT>), dim3(blocks), dim3(256), 0, s, X, ldx, W, b,
+    const int blocks = (M + kLdsBM - 1) / kLdsBM;
+    hipLaunchKernelGGL((xent_fwd_kernel<V, NT>), dim3(blocks), dim3(256), 0, s, X, ldx, W, b,
                        labels, M, K, C, 1.0f / (float)M, G, ldg, loss_part, db_part, logits, ldl);
     return hipGetLastError();
 }
@@ -308,7 +300,7 @@ hipError_t launch_dw(const float *X, int64_t ldx, const float *G, int ldg, int M
 int64_t xent_workspace_bytes(int64_t M, int64_t K, int64_t C) {
     if (M <= 0 || K <= 0 || C <= 0) return 0;
     const int64_t C16 = (C + 15) / 16 * 16;
-    const int64_t waves = (M + 16 * kXentMT - 1) / (16 * kXentMT);
+    const int64_t waves = (M + kLdsBM - 1) / kLdsBM * 4;
     const int64_t n_slabs = std::min<int64_t>(512, (M + 255) / 256);
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     return al(M * C16 * 4) + al(waves * 8) + al(waves * C16 * 4) + al(n_slabs * C16 * K * 4) + 512;
@@ -329,7 +321,7 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
                 (long long)ws_bytes, (long long)need);
     const int NT = (int)((C + 15) / 16);
     const int C16 = NT * 16;
-    const int waves = (int)((M + 16 * kXentMT - 1) / (16 * kXentMT));
+    const int waves = (int)((M + kLdsBM - 1) / kLdsBM * 4);
     const int n_slabs = (int)std::min<int64_t>(512, (M + 255) / 256);
     const int rows_per = (int)(((M + n_slabs - 1) / n_slabs + 3) / 4 * 4);
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
