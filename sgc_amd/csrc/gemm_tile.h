@@ -87,8 +87,13 @@ namespace sgc {
 // streaming its own W rows (xwt_tile), W leaves L2 once per block, not once
 // per wave, and X arrives in whole 128-B lines.
 constexpr int kLdsBM = 128;
-constexpr int kLdsBK = 32;
-constexpr int kLdsPad = kLdsBK + 1;  // row stride in LDS: conflict-free ds_read_b32 columns
+#ifndef SGC_LDS_BK
+#define SGC_LDS_BK 32
+#endif
+constexpr int kLdsBK = SGC_LDS_BK;
+// LDS row stride == 2 (mod 32): the 32 lanes of a ds_read_b32 half-wave (16
+// rows x 2 adjacent k) then hit 32 distinct banks.
+constexpr int kLdsPad = kLdsBK + 2;
 
 template <int V, int NT>
 struct LdsTile {
