@@ -8,7 +8,8 @@ one sgc_precompute (all K hops of S.X, reference utils.py:92-97) over the
 synthetic Reddit-shape graph (232,965 nodes, 11,606,919 undirected edges,
 nnz(S) = 23,446,803, F = 602, K = 2), inputs resident in HBM.
 A "step" = one full K-hop propagation.  N > 1: S row-partitioned over ranks
-(nnz-balanced), one RCCL all-gather of X per hop (sgc_amd.distributed);
+(equal-row blocks), one RCCL all-gather of X per hop, pipelined in feature
+groups (sgc_amd.distributed);
 total work is fixed, so scaling is "strong".
 
 Also printed (same JSON line):
@@ -112,6 +113,8 @@ def main():
                     help="N>1: feature-group width of the compute/all-gather pipeline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged rehearsal of the N>1 path (ranks may share a GPU)")
+    ap.add_argument("--distributed-path", action="store_true",
+                    help="run the row-partitioned path even at N=1 (exercises RCCL on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,7 +126,12 @@ def main():
     local_dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    if world > 1:
+    distributed = world > 1 or args.distributed_path
+    if distributed:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29555")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
         else:
@@ -138,13 +146,13 @@ def main():
     n, F, nnz = S.n, X_host.shape[1], S.nnz
     X0 = torch.from_numpy(X_host).to(dev)
 
-    n_launch = args.steps * K * (1 if world == 1 else -(-(F + 31) // 32 * 32 // max(2, args.group_floats)))
+    n_launch = args.steps * K * (1 if not distributed else -(-(F + 31) // 32 * 32 // max(2, args.group_floats)))
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(n_launch)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(n_launch)]
     launch_bytes = []
     ev = {"i": 0, "on": False}
 
-    if world == 1:
+    if not distributed:
         csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
         csr.plan(0, n, args.threshold)
         out_buf = torch.empty((n, F), device=dev)
@@ -191,7 +199,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     ev["on"] = True
@@ -199,13 +207,13 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     ev["on"] = False
     kern_ms = [s.elapsed_time(e) for s, e in zip(starts[:ev["i"]], ends[:ev["i"]])]
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
@@ -213,7 +221,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     value = K * nnz * args.steps / elapsed
     kern_mean_ms = float(np.mean(kern_ms)) if kern_ms else float("nan")
-    if world == 1:
+    if not distributed:
         bytes_launch = algorithmic_bytes_per_hop(n, nnz, F)
         unit_desc = f"one hop over all {n} rows"
     else:
@@ -221,7 +229,7 @@ def main():
         unit_desc = (f"one hop of one {args.group_floats}-float feature group over rank 0's "
                      f"{shard.rows} rows ({nnz_l} nnz)")
     achieved = bytes_launch / (kern_mean_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(args.shape) if world == 1 else (None, None)
+    traffic, traffic_src = load_traffic(args.shape) if not distributed else (None, None)
 
     rec = None
     if rank == 0:
@@ -251,10 +259,10 @@ def main():
                          "compulsory_bytes_per_hop": 4 * (n + 1) + 8 * nnz + 8 * F * n},
             "generate_seconds": round(t_gen, 2),
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not distributed and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(S, X_host)
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -32,6 +32,13 @@
 #include <string>
 #include <vector>
 
+#ifndef SGC_NT_STORE
+#define SGC_NT_STORE 0
+#endif
+#ifndef SGC_NT_META
+#define SGC_NT_META 0
+#endif
+
 namespace sgc {
 
 // Accumulate the C chunks [chunk0, chunk0 + C) of one row and store them.
@@ -64,8 +71,13 @@ __device__ __forceinline__ void row_chunks(const int *__restrict__ col,
         int my_col = 0;
         float my_val = 0.0f;
         if (lane < n) {
+#if SGC_NT_META
+            my_col = __builtin_nontemporal_load(col + base + lane);
+            my_val = __builtin_nontemporal_load(val + base + lane);
+#else
             my_col = col[base + lane];
             my_val = val[base + lane];
+#endif
         }
         // U nonzeros per step; the last step of a batch re-reads its last
         // valid nonzero for the missing ones (same lines, no extra traffic)
@@ -101,7 +113,17 @@ __device__ __forceinline__ void row_chunks(const int *__restrict__ col,
     char *Yb = reinterpret_cast<char *>(yrow);
 #pragma unroll
     for (int c = 0; c < C; ++c)
-        if (ok[c]) *reinterpret_cast<VT *>(Yb + boff[c]) = acc[c];
+        if (ok[c]) {
+#if SGC_NT_STORE
+            // streamed output: do not let Y rows displace hot X rows in L2
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                __builtin_nontemporal_store(lane_elem<V>(acc[c], v),
+                                            reinterpret_cast<float *>(Yb + boff[c]) + v);
+#else
+            *reinterpret_cast<VT *>(Yb + boff[c]) = acc[c];
+#endif
+        }
 }
 
 // Grid: x = work items of one feature slice, y = slice.  Workgroups are
