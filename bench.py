@@ -109,6 +109,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threshold", type=int, default=None, help="heavy-row threshold")
+    ap.add_argument("--hub-threshold", type=int, default=None, help="hub-row threshold")
     ap.add_argument("--group-floats", type=int, default=128,
                     help="N>1: feature-group width of the compute/all-gather pipeline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -154,7 +155,7 @@ def main():
 
     if not distributed:
         csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
-        csr.plan(0, n, args.threshold)
+        csr.plan(0, n, args.threshold, args.hub_threshold)
         out_buf = torch.empty((n, F), device=dev)
 
         def hook(phase, h):
@@ -167,7 +168,8 @@ def main():
                 ev["i"] += 1
 
         def step():  # the product path of sgc_precompute (sgc_amd.propagate)
-            return propagate(csr, X0, K, out=out_buf, threshold=args.threshold, hop_hook=hook)
+            return propagate(csr, X0, K, out=out_buf, threshold=args.threshold, hop_hook=hook,
+                             hub_threshold=args.hub_threshold)
         parallelism = "single-gpu"
     else:
         from sgc_amd.distributed import RowPartitionedPropagator, make_shard

@@ -107,20 +107,27 @@ int sgc_csr_to_coo64(const int32_t *row_ptr, const int32_t *col_idx, int64_t n_r
 
 /* ---------------------------------------------------------------------------
  * Schedule ("plan") for the SpMM.  Lists the rows of [row_begin, row_end)
- * with more than heavy_threshold nonzeros, heaviest first.  sgc_spmm_csr_f32
- * runs each listed row as one work item per 64V-float feature chunk (so a
- * power-law hub runs on several wavefronts at once, scheduled first) and
- * every other row as one work item.  The plan changes only the schedule:
- * every output element is still one sequential FMA chain, so results never
- * depend on it.  Synchronous (reads the heavy-row list back to sort it).
+ * with more than heavy_threshold nonzeros, heaviest first; the first n_hub
+ * of them have more than hub_threshold (>= heavy_threshold).
+ * sgc_spmm_csr_f32 runs
+ *   - each hub row on 1024-thread workgroups (one per 64-feature chunk; 15
+ *     waves gather nonzeros ahead into LDS, one runs the FMA chain), on a
+ *     side stream joined back to the caller's stream;
+ *   - each other heavy row as one wave per 128-float chunk, scheduled first;
+ *   - every remaining row as one wave.
+ * The plan changes only the schedule: every output element is still one
+ * sequential FMA chain, so results never depend on it.  Synchronous (reads
+ * the heavy-row list back to sort it).
  *
  * plan must hold sgc_plan_capacity(row_end - row_begin) int32 words;
- * *n_heavy_host receives the number of heavy rows written to plan[0..).
+ * *n_heavy_host receives the number of heavy rows written to plan[0..),
+ * *n_hub_host (may be NULL) how many of them lead as hub rows.
  * ------------------------------------------------------------------------- */
 int64_t sgc_plan_capacity(int64_t n_rows);
 int sgc_plan_build(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
-                   int32_t heavy_threshold, int32_t *plan, int64_t plan_capacity,
-                   int64_t *n_heavy_host, void *stream);
+                   int32_t heavy_threshold, int32_t hub_threshold, int32_t *plan,
+                   int64_t plan_capacity, int64_t *n_heavy_host, int64_t *n_hub_host,
+                   void *stream);
 
 /* ---------------------------------------------------------------------------
  * One hop Y = S[row_begin:row_end, :] . X  (utils.py:95, torch.spmm).
@@ -128,14 +135,14 @@ int sgc_plan_build(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
  *     acc = +0.0f; for k in row i (CSR order): acc = fmaf(val[k], X[col[k], f], acc)
  * -- bit-identical to the reference CPU kernel.  X rows have stride ldx
  * floats, Y rows ldy floats; X must not alias Y.
- * plan/n_heavy/heavy_threshold from sgc_plan_build over the same row range,
- * or plan = NULL (one work item per row, natural order).
+ * plan/n_heavy/n_hub/heavy_threshold from sgc_plan_build over the same row
+ * range, or plan = NULL (one work item per row, natural order).
  * ------------------------------------------------------------------------- */
 int sgc_spmm_csr_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                      int64_t row_begin, int64_t row_end,
                      const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
-                     const int32_t *plan, int64_t n_heavy, int32_t heavy_threshold,
-                     void *stream);
+                     const int32_t *plan, int64_t n_heavy, int64_t n_hub,
+                     int32_t heavy_threshold, void *stream);
 
 /* K hops X_K = S^K X_0 over all n_rows rows (utils.py:92-97, the whole
  * sgc_precompute loop).  out (row stride ldo) receives X_K.  Intermediate
@@ -150,8 +157,9 @@ int64_t sgc_propagate_workspace(int64_t n_rows, int64_t F, int64_t ldx, int32_t 
 int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                       int64_t n_rows, const float *X0, int64_t ldx, float *out,
                       int64_t ldo, int64_t F, int32_t K,
-                      const int32_t *plan, int64_t n_heavy, int32_t heavy_threshold,
-                      void *workspace, int64_t workspace_bytes, void *stream);
+                      const int32_t *plan, int64_t n_heavy, int64_t n_hub,
+                      int32_t heavy_threshold, void *workspace, int64_t workspace_bytes,
+                      void *stream);
 
 /* Row-strided copy dst[i, 0:F] = src[i, 0:F] (re-layout of feature rows). */
 int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd,

@@ -25,7 +25,8 @@ from sgc_amd.propagate import DeviceCSR  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--libs", default="")
-    ap.add_argument("--thresholds", default="512")
+    ap.add_argument("--thresholds", default="2048")
+    ap.add_argument("--hubs", default="4096", help="hub thresholds (sgc_plan_build)")
     ap.add_argument("--slices", default="128", help="slice_floats values (sgc_set_tuning)")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=3)
@@ -41,7 +42,8 @@ def main():
     F = graphs.SHAPES[args.shape]["features"]
     X = torch.from_numpy(graphs.synthetic_features(args.shape, S.n, F, seed=1)).to(dev)
     csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
-    plans = {t: csr.plan(0, S.n, t) for t in thresholds}
+    hubs = [int(x) for x in args.hubs.split(",")]
+    plans = {(t, hb): csr.plan(0, S.n, t, hb) for t in thresholds for hb in hubs}
     Y = torch.empty_like(X)
     lds = [int(x) or F for x in args.ld.split(",")]
     Xs = {}
@@ -52,20 +54,20 @@ def main():
     stream = _lib.stream_handle(dev)
     ref = None
     slices = [int(x) for x in args.slices.split(",")]
-    variants = [(f"{name}/s{sf}/ld{ld}", lib, t, (sf, ld)) for name, lib in loaded
-                for t in thresholds for sf in slices for ld in lds]
+    variants = [(f"{name}/s{sf}/ld{ld}/hub{hb}", lib, t, (sf, ld, hb)) for name, lib in loaded
+                for t in thresholds for sf in slices for ld in lds for hb in hubs]
 
     def run(lib, t, cfg):
-        sf, ld = cfg
+        sf, ld, hb = cfg
         lib.sgc_set_tuning(b"slice_floats", sf)
-        plan, nh, thr = plans[t]
+        pl = plans[(t, hb)]
         rc = lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val),
-                                  0, S.n, _lib.ptr(Xs[ld]), ld, _lib.ptr(Y), F, F, _lib.ptr(plan),
-                                  nh, thr, stream)
+                                  0, S.n, _lib.ptr(Xs[ld]), ld, _lib.ptr(Y), F, F, _lib.ptr(pl.rows),
+                                  pl.n_heavy, pl.n_hub, pl.threshold, stream)
         if rc:
             raise RuntimeError(lib.sgc_last_error())
 
-    times = {(n, t): [] for n, _, t, _ in variants}
+    times = {(n, t): [] for n, _, t, _ in variants}  # n encodes slice/ld/hub
     for name, lib, t, sf in variants:  # warm-up + correctness
         run(lib, t, sf)
         torch.cuda.synchronize()

@@ -34,12 +34,13 @@ SIGNATURES = {
                                         ctypes.POINTER(_i64), _p]),
     "sgc_csr_to_coo64": (ctypes.c_int, [_p, _p, _i64, _p, _p, _p]),
     "sgc_plan_capacity": (_i64, [_i64]),
-    "sgc_plan_build": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, ctypes.POINTER(_i64), _p]),
+    "sgc_plan_build": (ctypes.c_int, [_p, _i64, _i64, _i32, _i32, _p, _i64, ctypes.POINTER(_i64),
+                                      ctypes.POINTER(_i64), _p]),
     "sgc_spmm_csr_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
-                                        _p, _i64, _i32, _p]),
+                                        _p, _i64, _i64, _i32, _p]),
     "sgc_propagate_workspace": (_i64, [_i64, _i64, _i64, _i32]),
     "sgc_propagate_f32": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _i32,
-                                         _p, _i64, _i32, _p, _i64, _p]),
+                                         _p, _i64, _i64, _i32, _p, _i64, _p]),
     "sgc_pad_rows_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i64, _p]),
     "sgc_aligned_ld": (_i64, [_i64]),
     "sgc_linear_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),

@@ -24,11 +24,12 @@ int csr64_to_csr(const int64_t *crow, const int64_t *col, const float *vals, int
                  int64_t n_rows, int64_t n_cols, int32_t *row_ptr, int32_t *col_idx,
                  float *val_out, uint32_t *status_host, hipStream_t stream);
 int build_plan(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int32_t threshold,
-               int32_t *plan, int64_t capacity, int64_t *n_heavy_host, hipStream_t stream);
+               int32_t hub_threshold, int32_t *plan, int64_t capacity, int64_t *n_heavy_host,
+               int64_t *n_hub_host, hipStream_t stream);
 int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                 int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
                 int64_t ldy, int64_t F, const int32_t *heavy_rows, int64_t n_heavy,
-                int32_t heavy_threshold, hipStream_t stream);
+                int64_t n_hub, int32_t heavy_threshold, hipStream_t stream);
 int launch_pad_rows(const float *src, int64_t lds, float *dst, int64_t ldd, int64_t n_rows,
                     int64_t F, hipStream_t stream);
 size_t augnorm_scan_temp_bytes(int64_t n);
@@ -116,18 +117,19 @@ int sgc_csr_to_coo64(const int32_t *row_ptr, const int32_t *col_idx, int64_t n_r
 int64_t sgc_plan_capacity(int64_t n_rows) { return 2 * (n_rows < 0 ? 0 : n_rows) + 1; }
 
 int sgc_plan_build(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
-                   int32_t heavy_threshold, int32_t *plan, int64_t plan_capacity,
-                   int64_t *n_heavy_host, void *stream) {
-    return build_plan(row_ptr, row_begin, row_end, heavy_threshold, plan, plan_capacity,
-                      n_heavy_host, as_stream(stream));
+                   int32_t heavy_threshold, int32_t hub_threshold, int32_t *plan,
+                   int64_t plan_capacity, int64_t *n_heavy_host, int64_t *n_hub_host,
+                   void *stream) {
+    return build_plan(row_ptr, row_begin, row_end, heavy_threshold, hub_threshold, plan,
+                      plan_capacity, n_heavy_host, n_hub_host, as_stream(stream));
 }
 
 int sgc_spmm_csr_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                      int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
                      int64_t ldy, int64_t F, const int32_t *plan, int64_t n_heavy,
-                     int32_t heavy_threshold, void *stream) {
+                     int64_t n_hub, int32_t heavy_threshold, void *stream) {
     return launch_spmm(row_ptr, col_idx, val, row_begin, row_end, X, ldx, Y, ldy, F, plan,
-                       plan ? n_heavy : 0, heavy_threshold, as_stream(stream));
+                       plan ? n_heavy : 0, plan ? n_hub : 0, heavy_threshold, as_stream(stream));
 }
 
 int64_t sgc_aligned_ld(int64_t F) { return F <= 0 ? 0 : (F + 31) / 32 * 32; }
@@ -150,7 +152,7 @@ int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int
 
 int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                       int64_t n_rows, const float *X0, int64_t ldx, float *out, int64_t ldo,
-                      int64_t F, int32_t K, const int32_t *plan, int64_t n_heavy,
+                      int64_t F, int32_t K, const int32_t *plan, int64_t n_heavy, int64_t n_hub,
                       int32_t heavy_threshold, void *workspace, int64_t workspace_bytes,
                       void *stream) {
     hipStream_t s = as_stream(stream);
@@ -184,7 +186,7 @@ int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const floa
         float *dst = last ? out : bufs[next];
         const int64_t ldd = last ? ldo : ldw;
         const int rc = launch_spmm(row_ptr, col_idx, val, 0, n_rows, src, lds, dst, ldd, F, plan,
-                                   plan ? n_heavy : 0, heavy_threshold, s);
+                                   plan ? n_heavy : 0, plan ? n_hub : 0, heavy_threshold, s);
         if (rc) return rc;
         src = dst;
         lds = ldd;

@@ -29,6 +29,8 @@
 #include "common.h"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -164,8 +166,78 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     if (r >= n_rows) return;
     const int row = row_begin + r;
     const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
-    if (n_heavy > 0 && k1 - k0 > heavy_threshold) return;  // done as heavy items
+    if (k1 - k0 > heavy_threshold) return;  // done as a heavy item or by the hub kernel
     row_chunks<V, C, U>(col, val, k0, k1, X, ldx, Y + (int64_t)r * ldy, F, slice * C, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Hub rows (degree > hub_threshold): one 1024-thread workgroup per (row,
+// 64-feature chunk).  A single wave's FMA chain over d nonzeros costs d FMAs
+// -- cheap -- but a wave keeps only ~16 nonzeros' X segments in flight, so a
+// 48k-nonzero hub on one wave runs ~3 ms, longer than a whole hop at P >= 2
+// GPUs.  Here 15 loader waves gather the next 240 nonzeros' 256-B X segments
+// (registers -> LDS, double buffered) while wave 0 runs the sequential
+// chain out of LDS: ~60 KB in flight per hub chunk, the same FMA order.
+constexpr int kHubChunk = 64;
+constexpr int kHubLoaders = 15;
+constexpr int kHubPerLoader = 16;
+constexpr int kHubRound = kHubLoaders * kHubPerLoader;  // 240 nonzeros per round
+
+__global__ __launch_bounds__(1024) void spmm_hub_kernel(
+    const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
+    const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy, int row_begin,
+    int F, const int *__restrict__ hub_rows, int n_chunks) {
+    __shared__ float gx[2][kHubRound][kHubChunk];  // 120 KB
+    __shared__ float gv[2][kHubRound];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    const int h = blockIdx.x / n_chunks;
+    const int c = blockIdx.x - h * n_chunks;
+    const int row = hub_rows[h];
+    const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
+    const int f = c * kHubChunk + lane;
+    const uint32_t boff = (f < F ? (uint32_t)f : 0u) * 4u;
+    const char *Xb = reinterpret_cast<const char *>(X);
+    const int64_t row_bytes = ldx * 4;
+    const int n_round = (k1 - k0 + kHubRound - 1) / kHubRound;
+    float regs[kHubPerLoader];
+    float vreg = 0.f;
+    auto load = [&](int r) {  // loader waves only; wave-uniform k
+        const int kb = k0 + r * kHubRound + (w - 1) * kHubPerLoader;
+#pragma unroll
+        for (int j = 0; j < kHubPerLoader; ++j) {
+            const int k = min(kb + j, k1 - 1);
+            const int cj = col[k];
+            regs[j] = *reinterpret_cast<const float *>(Xb + (int64_t)cj * row_bytes + boff);
+        }
+        const int kl = min(kb + (lane & (kHubPerLoader - 1)), k1 - 1);
+        vreg = val[kl];
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < kHubPerLoader; ++j) gx[buf][(w - 1) * kHubPerLoader + j][lane] = regs[j];
+        if (lane < kHubPerLoader) gv[buf][(w - 1) * kHubPerLoader + lane] = vreg;
+    };
+    if (w > 0 && n_round > 0) {
+        load(0);
+        store(0);
+    }
+    __syncthreads();
+    float acc = 0.0f;
+    for (int r = 0; r < n_round; ++r) {
+        const int buf = r & 1;
+        if (w > 0) {
+            if (r + 1 < n_round) {
+                load(r + 1);
+                store(buf ^ 1);
+            }
+        } else {
+            const int n = min(kHubRound, k1 - (k0 + r * kHubRound));
+            for (int kk = 0; kk < n; ++kk) acc = __builtin_fmaf(gv[buf][kk], gx[buf][kk][lane], acc);
+        }
+        __syncthreads();
+    }
+    if (w == 0 && f < F) Y[(int64_t)(row - row_begin) * ldy + f] = acc;
 }
 
 namespace {
@@ -187,6 +259,31 @@ struct LaunchArgs {
     int slices;
     hipStream_t stream;
 };
+
+// A side stream + fork/join events per device for the hub kernel (runs beside
+// the main kernel; ordered against the caller's stream by events, so the pair
+// is capturable into a hipGraph).
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+
+hipError_t side_stream(SideStream **out) {
+    static std::mutex mu;
+    static std::map<int, SideStream> per_dev;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    SideStream &ss = per_dev[dev];
+    if (!ss.s) {
+        if ((e = hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    *out = &ss;
+    return hipSuccess;
+}
 
 // Nonzeros in flight per wave: light items keep U*C*V <= ~40 registers of
 // gathered X; heavy sub-chunk items (one float per lane) go deeper (UH).
@@ -267,7 +364,7 @@ int64_t get_tuning(const char *key) {
 int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                 int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
                 int64_t ldy, int64_t F, const int32_t *heavy_rows, int64_t n_heavy,
-                int32_t heavy_threshold, hipStream_t stream) {
+                int64_t n_hub, int32_t heavy_threshold, hipStream_t stream) {
     SGC_REQUIRE(row_ptr && col_idx && val && X && Y, SGC_EINVAL, "spmm: null pointer");
     SGC_REQUIRE(row_begin >= 0 && row_end >= row_begin && row_end < INT32_MAX, SGC_ERANGE,
                 "spmm: bad row range [%lld, %lld)", (long long)row_begin, (long long)row_end);
@@ -277,7 +374,26 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     SGC_REQUIRE(n_heavy >= 0 && (n_heavy == 0 || heavy_rows), SGC_EINVAL, "spmm: bad plan");
     const int64_t n_rows = row_end - row_begin;
     if (n_rows == 0) return SGC_OK;
-    if (!heavy_rows) n_heavy = 0;
+    if (!heavy_rows) {
+        n_heavy = 0;
+        heavy_threshold = INT32_MAX;  // no plan: every row is a light item
+    }
+    n_hub = std::max<int64_t>(0, std::min<int64_t>(n_hub, n_heavy));
+    SideStream *side = nullptr;
+    if (n_hub > 0) {
+        // hub rows (the heaviest n_hub of the plan) run on the side stream
+        const int n_chunks = (int)((F + kHubChunk - 1) / kHubChunk);
+        SGC_REQUIRE(n_hub * n_chunks < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many hub items");
+        SGC_HIP_CHECK(side_stream(&side));
+        SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
+        SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
+        hipLaunchKernelGGL(spmm_hub_kernel, dim3((unsigned)(n_hub * n_chunks)), dim3(1024), 0,
+                           side->s, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)F,
+                           heavy_rows, n_chunks);
+        SGC_HIP_CHECK(hipGetLastError());
+        heavy_rows += n_hub;
+        n_heavy -= n_hub;
+    }
 
     const int V = pick_vec(F, ldx, ldy, X, Y);
     const int chunks_total = (int)((F + kWave * V - 1) / (kWave * V));
@@ -299,6 +415,10 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     else
         e = dispatch_c<1, max_chunks(1)>(C, a);
     SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "spmm launch failed: %s", hipGetErrorString(e));
+    if (side) {  // join: the caller's stream waits for the hub kernel
+        SGC_HIP_CHECK(hipEventRecord(side->join, side->s));
+        SGC_HIP_CHECK(hipStreamWaitEvent(stream, side->join, 0));
+    }
     return SGC_OK;
 }
 
@@ -358,9 +478,11 @@ __global__ void heavy_rows_kernel(const int *__restrict__ row_ptr, int row_begin
 }
 
 int build_plan(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
-               int32_t threshold, int32_t *plan, int64_t capacity, int64_t *n_heavy_host,
-               hipStream_t stream) {
+               int32_t threshold, int32_t hub_threshold, int32_t *plan, int64_t capacity,
+               int64_t *n_heavy_host, int64_t *n_hub_host, hipStream_t stream) {
     SGC_REQUIRE(row_ptr && plan && n_heavy_host, SGC_EINVAL, "plan: null pointer");
+    SGC_REQUIRE(hub_threshold >= threshold, SGC_EINVAL, "plan: hub_threshold < heavy_threshold");
+    if (n_hub_host) *n_hub_host = 0;
     const int64_t n_rows = row_end - row_begin;
     SGC_REQUIRE(n_rows >= 0 && row_end < INT32_MAX, SGC_ERANGE, "plan: bad row range");
     SGC_REQUIRE(capacity >= 2 * n_rows + 1, SGC_ENOMEM, "plan: capacity %lld < %lld",
@@ -385,7 +507,12 @@ int build_plan(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
         for (int i = 0; i < h; ++i) dr[i] = {-pairs[2 * i], pairs[2 * i + 1]};
         std::sort(dr.begin(), dr.end());  // degree desc, then row asc
         std::vector<int> rows(h);
-        for (int i = 0; i < h; ++i) rows[i] = dr[i].second;
+        int64_t hubs = 0;
+        for (int i = 0; i < h; ++i) {
+            rows[i] = dr[i].second;
+            hubs += (-dr[i].first > hub_threshold);
+        }
+        if (n_hub_host) *n_hub_host = hubs;
         SGC_HIP_CHECK(hipMemcpyAsync(plan, rows.data(), h * sizeof(int), hipMemcpyHostToDevice,
                                      stream));
         SGC_HIP_CHECK(hipStreamSynchronize(stream));

@@ -6,15 +6,27 @@ utils.py:92-97).  Host code only marshals torch tensors into the C ABI
 """
 import os
 from dataclasses import dataclass, field
-from typing import Optional
+from typing import NamedTuple, Optional
 
 import torch
 
 from . import _lib
 
 # Rows with more nonzeros than this are split into per-feature-chunk work
-# items and scheduled first (see sgc_plan_build).  Results never depend on it.
+# items and scheduled first; rows above the hub threshold run on the LDS-
+# staged hub kernel (see sgc_plan_build).  Results never depend on either.
 DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SGC_AMD_HEAVY_THRESHOLD", "2048"))
+DEFAULT_HUB_THRESHOLD = int(os.environ.get("SGC_AMD_HUB_THRESHOLD", "4096"))
+
+
+class Plan(NamedTuple):
+    rows: Optional[torch.Tensor]  # int32 heavy rows, heaviest first (None: no plan)
+    n_heavy: int
+    n_hub: int
+    threshold: int
+
+
+NO_PLAN = Plan(None, 0, 0, 0)
 
 STATUS_ROWS_SORTED = 1
 STATUS_COLS_ASCENDING = 2
@@ -115,23 +127,26 @@ class DeviceCSR:
         csr.ingest_seconds = time.perf_counter() - t0
         return csr
 
-    def plan(self, row_begin=0, row_end=None, threshold=None):
+    def plan(self, row_begin=0, row_end=None, threshold=None, hub_threshold=None) -> Plan:
         """Heavy-row schedule for rows [row_begin, row_end) (cached)."""
         row_end = self.n_rows if row_end is None else row_end
         threshold = DEFAULT_HEAVY_THRESHOLD if threshold is None else int(threshold)
-        key = (row_begin, row_end, threshold)
+        hub = DEFAULT_HUB_THRESHOLD if hub_threshold is None else int(hub_threshold)
+        hub = max(hub, threshold)
+        key = (row_begin, row_end, threshold, hub)
         if key not in self._plans:
             lib = _lib.load()
             n = row_end - row_begin
             cap = lib.sgc_plan_capacity(n)
             buf = torch.empty(max(1, cap), dtype=torch.int32, device=self.device)
-            n_heavy = _lib._i64(0)
+            n_heavy, n_hub = _lib._i64(0), _lib._i64(0)
             with torch.cuda.device(self.device):
                 _lib.check(lib.sgc_plan_build(_lib.ptr(self.row_ptr), row_begin, row_end, threshold,
-                                              _lib.ptr(buf), cap, ctypes_byref(n_heavy),
+                                              hub, _lib.ptr(buf), cap, ctypes_byref(n_heavy),
+                                              ctypes_byref(n_hub),
                                               _lib.stream_handle(self.device)), "plan_build")
             h = int(n_heavy.value)
-            self._plans[key] = (buf[:max(h, 1)].clone(), h, threshold)
+            self._plans[key] = Plan(buf[:max(h, 1)].clone(), h, int(n_hub.value), threshold)
         return self._plans[key]
 
 
@@ -187,7 +202,7 @@ def _check_features(X, csr):
 
 
 def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
-         use_plan=True, threshold=None):
+         use_plan=True, threshold=None, hub_threshold=None):
     """One hop Y = S[row_begin:row_end] . X (bit-exact with torch.spmm on CPU)."""
     X = _check_features(X, csr)
     row_end = csr.n_rows if row_end is None else row_end
@@ -196,13 +211,13 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
         out = torch.empty((row_end - row_begin, F), dtype=torch.float32, device=X.device)
     if F == 0 or row_end == row_begin:
         return out
-    plan, n_heavy, thr = csr.plan(row_begin, row_end, threshold) if use_plan else (None, 0, 0)
+    pl = csr.plan(row_begin, row_end, threshold, hub_threshold) if use_plan else NO_PLAN
     lib = _lib.load()
     with torch.cuda.device(X.device):
         _lib.check(lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
                                         _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
                                         X.stride(0), _lib.ptr(out), out.stride(0), F,
-                                        _lib.ptr(plan), n_heavy, thr,
+                                        _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
                                         _lib.stream_handle(X.device)), "spmm_csr_f32")
     return out
 
@@ -217,7 +232,7 @@ def _needs_pad(X):
 
 
 def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, threshold=None,
-              hop_hook=None, native_loop=False):
+              hop_hook=None, native_loop=False, hub_threshold=None):
     """X_K = S^K X on the device (K >= 1); asynchronous on the current stream.
 
     Mirrors sgc_propagate_f32: X is first re-laid into 128-B aligned rows when
@@ -236,7 +251,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
         if K <= 0:
             out.copy_(X)
         return out
-    plan, n_heavy, thr = csr.plan(0, n, threshold) if use_plan else (None, 0, 0)
+    pl = csr.plan(0, n, threshold, hub_threshold) if use_plan else NO_PLAN
     lib = _lib.load()
     stream = _lib.stream_handle(X.device)
     ldw = aligned_ld(F)
@@ -247,8 +262,8 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
             _lib.check(lib.sgc_propagate_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
                                              _lib.ptr(csr.val), n, _lib.ptr(X), X.stride(0),
                                              _lib.ptr(out), out.stride(0), F, int(K),
-                                             _lib.ptr(plan), n_heavy, thr, _lib.ptr(ws), ws_bytes,
-                                             stream), "propagate_f32")
+                                             _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
+                                             _lib.ptr(ws), ws_bytes, stream), "propagate_f32")
             return out
         bufs = [torch.empty((n, ldw), dtype=torch.float32, device=X.device)
                 for _ in range(2 if K >= 2 else 1)]
@@ -263,8 +278,9 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                 hop_hook("start", h)
             _lib.check(lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
                                             _lib.ptr(csr.val), 0, n, _lib.ptr(src), src.stride(0),
-                                            _lib.ptr(dst), dst.stride(0), F, _lib.ptr(plan),
-                                            n_heavy, thr, stream), "spmm_csr_f32")
+                                            _lib.ptr(dst), dst.stride(0), F, _lib.ptr(pl.rows),
+                                            pl.n_heavy, pl.n_hub, pl.threshold, stream),
+                       "spmm_csr_f32")
             if hop_hook:
                 hop_hook("end", h)
             src, nxt = dst, nxt ^ 1

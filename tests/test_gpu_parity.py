@@ -54,19 +54,21 @@ def test_tiny_cases_sgc_precompute_bit_exact(tiny_cases):
             assert bits_equal(out.cpu().numpy(), c[key]), (name, K)
 
 
-@pytest.mark.parametrize("threshold", [0, 1, 7, 63, 10**9])
-def test_heavy_split_schedule_never_changes_bits(tiny_cases, threshold):
-    """Every row as heavy items (threshold 0) .. no heavy rows: same bits."""
+@pytest.mark.parametrize("threshold,hub", [(0, 0), (1, 7), (7, 7), (63, 500), (0, 10**9),
+                                           (10**9, 10**9), (2048, 4096)])
+def test_heavy_split_schedule_never_changes_bits(tiny_cases, threshold, hub):
+    """Every row a hub (0, 0), every row heavy (0, inf) .. no heavy rows: same bits."""
     from sgc_amd.propagate import DeviceCSR, propagate
     for name in ("hub1000_F65", "hub1000_F130", "norm_n48_F602", "norm_n48_F130",
-                 "norm_n48_F3", "raw_sorted_dups_F66"):
+                 "norm_n48_F3", "raw_sorted_dups_F66", "raw_unsorted_dups_F7", "special_values_F11",
+                 "isolated_F17"):
         c = tiny_cases[name]
         csr = DeviceCSR.from_torch(coo_cuda(c))
         X = torch.from_numpy(c["X"]).to(DEV)
         for key in sorted(k for k in c if k.startswith("Y") and k != "Y0"):
-            out = propagate(csr, X, int(key[1:]), threshold=threshold)
+            out = propagate(csr, X, int(key[1:]), threshold=threshold, hub_threshold=hub)
             torch.cuda.synchronize()
-            assert bits_equal(out.cpu().numpy(), c[key]), (name, key, threshold)
+            assert bits_equal(out.cpu().numpy(), c[key]), (name, key, threshold, hub)
 
 
 def test_no_plan_path(tiny_cases):
@@ -106,7 +108,7 @@ def test_row_slices_and_strides(tiny_cases):
     for lo, hi in ((0, 5), (5, 31), (31, 48), (10, 10)):
         for Xin in (X, Xpad[:, :602]):
             out = torch.full((hi - lo, 700), float("nan"), device=DEV)
-            spmm(csr, Xin, lo, hi, out=out[:, :602], threshold=3)
+            spmm(csr, Xin, lo, hi, out=out[:, :602], threshold=3, hub_threshold=5)
             torch.cuda.synchronize()
             o = out.cpu().numpy()
             assert bits_equal(o[:, :602], full[lo:hi])
