@@ -7,10 +7,19 @@ Metric (BASELINE.json): propagated edges/s = hops * nnz(S) / t, where t is
 one sgc_precompute (all K hops of S.X, reference utils.py:92-97) over the
 synthetic Reddit-shape graph (232,965 nodes, 11,606,919 undirected edges,
 nnz(S) = 23,446,803, F = 602, K = 2), inputs resident in HBM.
-A "step" = one full K-hop propagation.  N > 1: S row-partitioned over ranks
-(equal-row blocks), one RCCL all-gather of X per hop, pipelined in feature
-groups (sgc_amd.distributed);
-total work is fixed, so scaling is "strong".
+A "step" = one full K-hop propagation.  N > 1 (sgc_amd.distributed), total
+work fixed, so scaling is "strong":
+  --partition rows (default)  S row-partitioned (equal-row blocks, SURVEY.md
+                8(e)); RCCL all-gather of X_k after each hop that feeds another,
+                pipelined in 128-float feature groups
+  --partition features  each rank runs all K hops on its block of feature
+                columns over the full S, no exchange between hops
+  --output sharded (default)  each rank ends with its row block of X_K -- the
+                layout the data-parallel classifier consumes
+                (sgc_amd.distributed.ShardedSGCTrainer); no gather after the
+                last hop (rows) / one all-to-all (features)
+  --output replicated  every rank ends with all of X_K (one more all-gather)
+The other output mode is timed too (`alt_output`, --alt-steps).
 
 Also printed (same JSON line):
   roofline      dominant kernel (the CSR SpMM) -- algorithmic bytes per hop
@@ -99,6 +108,124 @@ def load_traffic(shape):
     return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
 
 
+def build_step(args, S, X0, dev, rank, world, distributed, K, output, timing):
+    """(step, parallelism, launch description) for one output mode.  timing =
+    {"on", "starts", "ends", "bytes"}: every SpMM launch is bracketed by HIP
+    events on its stream while timing["on"]."""
+    n, F = X0.shape
+
+    def bracket(fn, nbytes):
+        def run(*a, **k):
+            if not timing["on"]:
+                return fn(*a, **k)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = fn(*a, **k)
+            e.record()
+            timing["starts"].append(s)
+            timing["ends"].append(e)
+            timing["bytes"].append(nbytes(*a))
+            return r
+        return run
+
+    if not distributed:
+        csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
+        csr.plan(0, n, args.threshold, args.hub_threshold)
+        out_buf = torch.empty((n, F), device=dev)
+        ev = {}
+
+        def hook(phase, h):
+            if not timing["on"]:
+                return
+            if phase == "start":
+                ev["s"] = torch.cuda.Event(enable_timing=True)
+                ev["s"].record()
+            else:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                timing["starts"].append(ev["s"])
+                timing["ends"].append(e)
+                timing["bytes"].append(algorithmic_bytes_per_hop(n, S.nnz, F))
+
+        def step():  # the product path of sgc_precompute (sgc_amd.propagate)
+            return propagate(csr, X0, K, out=out_buf, threshold=args.threshold, hop_hook=hook,
+                             hub_threshold=args.hub_threshold)
+        return step, "single-gpu", f"one hop over all {n} rows"
+
+    backend = "rccl" if args.dist_backend == "nccl" else "gloo rehearsal"
+    staging = args.dist_backend == "gloo"
+    if args.partition == "features":
+        from sgc_amd.distributed import FeaturePartitionedPropagator, feature_bounds
+        from sgc_amd.propagate import spmm as spmm_hip
+        csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
+        rp = np.asarray(S.row_ptr, dtype=np.int64)
+
+        def launch_bytes(X, r0, r1, out):
+            nz, w = int(rp[r1] - rp[r0]), X.shape[1]
+            return 4 * (r1 - r0 + 1) + 8 * nz + 4 * w * nz + 4 * w * (r1 - r0)
+
+        spmm_fn = bracket(lambda X, r0, r1, out: spmm_hip(
+            csr, X, r0, r1, out=out, threshold=args.threshold,
+            hub_threshold=args.hub_threshold), launch_bytes)
+        prop = FeaturePartitionedPropagator(csr, rank=rank, world_size=world, spmm_fn=spmm_fn,
+                                            chunks=args.chunks, host_staging=staging)
+        fb, fB = feature_bounds(F, world)
+        exch = ("one all-to-all of the row blocks of X_K" if output == "sharded" else
+                f"one all-gather of X_K pipelined with the last hop in {args.chunks} row chunks")
+        par = (f"feature-partition x{world} ({fB}-column blocks, all K hops local) + {backend} "
+               f"{exch}; output {output}")
+        unit = (f"rank 0's SpMM launches (mean): hops over all {n} rows or last-hop row blocks, "
+                f"{int(fb[1] - fb[0])} feature columns")
+    else:
+        from sgc_amd.distributed import RowPartitionedPropagator, _default_spmm, make_shard
+        shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
+        nnz_l = shard.nnz
+
+        def launch_bytes(sh, X, out):
+            fg = X.shape[1]
+            return 4 * (sh.rows + 1) + 8 * nnz_l + 4 * fg * nnz_l + 4 * fg * sh.rows
+
+        prop = RowPartitionedPropagator(shard, spmm_fn=bracket(_default_spmm, launch_bytes),
+                                        group_floats=args.group_floats, host_staging=staging)
+        exch = ("all-gather of X_k after each hop but the last" if output == "sharded" else
+                "all-gather of X_k after every hop")
+        par = (f"row-partition x{world} (equal-row blocks) + {backend} {exch}, pipelined in "
+               f"{args.group_floats}-float feature groups; output {output}")
+        unit = (f"one hop of one {args.group_floats}-float feature group over rank 0's "
+                f"{shard.rows} rows ({nnz_l} nnz)")
+    out = None
+    if output == "replicated":
+        out = torch.empty((n, F), device=dev)
+
+    def step():
+        return prop.propagate(X0, K, out=out, output=output)
+    return step, par, unit
+
+
+def timed(step, steps, warmup, distributed, dev, timing):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timing["on"] = True
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timing["on"] = False
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    return elapsed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,12 +237,20 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threshold", type=int, default=None, help="heavy-row threshold")
     ap.add_argument("--hub-threshold", type=int, default=None, help="hub-row threshold")
-    ap.add_argument("--group-floats", type=int, default=128,
-                    help="N>1: feature-group width of the compute/all-gather pipeline")
+    ap.add_argument("--group-floats", type=int, default=320,
+                    help="N>1 rows: feature-group width of the compute/all-gather pipeline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged rehearsal of the N>1 path (ranks may share a GPU)")
     ap.add_argument("--distributed-path", action="store_true",
-                    help="run the row-partitioned path even at N=1 (exercises RCCL on one GPU)")
+                    help="run the N>1 path even at N=1 (exercises RCCL on one GPU)")
+    ap.add_argument("--partition", default="rows", choices=["rows", "features"],
+                    help="N>1: split the rows of S (per-hop all-gather) or the feature columns")
+    ap.add_argument("--output", default="sharded", choices=["sharded", "replicated"],
+                    help="N>1: each rank keeps its row block of X_K, or all ranks get all of it")
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="N>1 features, replicated output: row chunks of the last hop")
+    ap.add_argument("--alt-steps", type=int, default=5,
+                    help="N>1: steps timed with the other output mode (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,91 +282,29 @@ def main():
     n, F, nnz = S.n, X_host.shape[1], S.nnz
     X0 = torch.from_numpy(X_host).to(dev)
 
-    n_launch = args.steps * K * (1 if not distributed else -(-(F + 31) // 32 * 32 // max(2, args.group_floats)))
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(n_launch)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(n_launch)]
-    launch_bytes = []
-    ev = {"i": 0, "on": False}
-
-    if not distributed:
-        csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
-        csr.plan(0, n, args.threshold, args.hub_threshold)
-        out_buf = torch.empty((n, F), device=dev)
-
-        def hook(phase, h):
-            if not ev["on"]:
-                return
-            if phase == "start":
-                starts[ev["i"]].record()
-            else:
-                ends[ev["i"]].record()
-                ev["i"] += 1
-
-        def step():  # the product path of sgc_precompute (sgc_amd.propagate)
-            return propagate(csr, X0, K, out=out_buf, threshold=args.threshold, hop_hook=hook,
-                             hub_threshold=args.hub_threshold)
-        parallelism = "single-gpu"
-    else:
-        from sgc_amd.distributed import RowPartitionedPropagator, make_shard
-        shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
-        from sgc_amd.distributed import _default_spmm
-
-        nnz_l = shard.nnz
-
-        def timed_spmm(sh, X, out):
-            if ev["on"]:
-                starts[ev["i"]].record()
-            r = _default_spmm(sh, X, out)
-            if ev["on"]:
-                ends[ev["i"]].record()
-                ev["i"] += 1
-                fg = X.shape[1]
-                launch_bytes.append(4 * (sh.rows + 1) + 8 * nnz_l + 4 * fg * nnz_l + 4 * fg * sh.rows)
-            return r
-        prop = RowPartitionedPropagator(shard, spmm_fn=timed_spmm, group_floats=args.group_floats,
-                                        host_staging=args.dist_backend == "gloo")
-        out_full = torch.empty((n, F), device=dev)
-
-        def step():
-            return prop.propagate(X0, K, out=out_full)
-        parallelism = (f"row-partition x{world} (equal-row blocks) + per-hop all-gather "
-                       f"({'rccl' if args.dist_backend == 'nccl' else 'gloo rehearsal'}), "
-                       f"pipelined in {args.group_floats}-float feature groups")
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev["on"] = True
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    ev["on"] = False
-    kern_ms = [s.elapsed_time(e) for s, e in zip(starts[:ev["i"]], ends[:ev["i"]])]
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    timing = {"on": False, "starts": [], "ends": [], "bytes": []}
+    step, parallelism, unit_desc = build_step(args, S, X0, dev, rank, world, distributed, K,
+                                              args.output, timing)
+    elapsed = timed(step, args.steps, args.warmup, distributed, dev, timing)
+    kern_ms = [s.elapsed_time(e) for s, e in zip(timing["starts"], timing["ends"])]
+    bytes_launch = float(np.mean(timing["bytes"])) if timing["bytes"] else float("nan")
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = K * nnz * args.steps / elapsed
     kern_mean_ms = float(np.mean(kern_ms)) if kern_ms else float("nan")
-    if not distributed:
-        bytes_launch = algorithmic_bytes_per_hop(n, nnz, F)
-        unit_desc = f"one hop over all {n} rows"
-    else:
-        bytes_launch = float(np.mean(launch_bytes)) if launch_bytes else float("nan")
-        unit_desc = (f"one hop of one {args.group_floats}-float feature group over rank 0's "
-                     f"{shard.rows} rows ({nnz_l} nnz)")
     achieved = bytes_launch / (kern_mean_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(args.shape) if not distributed else (None, None)
+
+    alt = None
+    if distributed and args.alt_steps > 0:
+        alt_mode = "replicated" if args.output == "sharded" else "sharded"
+        t_alt = {"on": False, "starts": [], "ends": [], "bytes": []}
+        alt_step, alt_par, _ = build_step(args, S, X0, dev, rank, world, distributed, K, alt_mode,
+                                          t_alt)
+        e_alt = timed(alt_step, args.alt_steps, 1, distributed, dev, t_alt)
+        alt = {"output": alt_mode, "parallelism": alt_par, "steps": args.alt_steps,
+               "ms_per_step": e_alt * 1e3 / args.alt_steps,
+               "value": K * nnz * args.alt_steps / e_alt}
 
     rec = None
     if rank == 0:
@@ -251,7 +324,8 @@ def main():
             "data": "synthetic (seeded R-MAT graph + AugNorm, SURVEY.md 8(d))",
             "config": {"workload": f"{args.shape}-shape sgc_precompute K={K}", "nodes": n,
                        "undirected_edges": spec["edges"], "nnz": nnz, "features": F, "hops": K,
-                       "parallelism": parallelism, "heavy_threshold": args.threshold},
+                       "parallelism": parallelism, "heavy_threshold": args.threshold,
+                       "hub_threshold": args.hub_threshold},
             "precompute_seconds": ms_per_step / 1e3,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -261,6 +335,8 @@ def main():
                          "compulsory_bytes_per_hop": 4 * (n + 1) + 8 * nnz + 8 * F * n},
             "generate_seconds": round(t_gen, 2),
         }
+        if alt is not None:
+            rec["alt_output"] = alt
         if world == 1 and not distributed and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(S, X_host)
         print(json.dumps(rec), flush=True)

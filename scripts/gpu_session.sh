@@ -19,16 +19,17 @@ run() {
 }
 for s in $STEPS; do
   case $s in
-    pytest) run pytest timeout -k 10 900 python -m pytest tests -x -q -m gpu ;;
+    pytest) run pytest timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    rankwork) run rankwork timeout -k 10 400 python scripts/rank_work.py ;;
     smoke)  run smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench timeout -k 10 600 python bench.py ${BENCH_ARGS} ;;
     aux)    run aux timeout -k 10 600 python scripts/bench_aux.py ;;
     rccl1)  run rccl1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 1 --steps 5 --warmup 2 \
-                --distributed-path --no-cpu-baseline ;;
+                --distributed-path --no-cpu-baseline ${DIST_ARGS} ;;
     dist)   run dist timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
-                --dist-backend gloo ;;
+                --dist-backend gloo ${DIST_ARGS} ;;
     prof)   cd /tmp && export TMPDIR=/tmp && \
             run prof timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
                 --output-format csv -- python3 "$ROOTDIR/bench.py" --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS}

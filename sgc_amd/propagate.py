@@ -15,8 +15,20 @@ from . import _lib
 # Rows with more nonzeros than this are split into per-feature-chunk work
 # items and scheduled first; rows above the hub threshold run on the LDS-
 # staged hub kernel (see sgc_plan_build).  Results never depend on either.
-DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SGC_AMD_HEAVY_THRESHOLD", "2048"))
-DEFAULT_HUB_THRESHOLD = int(os.environ.get("SGC_AMD_HUB_THRESHOLD", "4096"))
+DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SGC_AMD_HEAVY_THRESHOLD", "512"))
+# Hub threshold: by default a row is a hub when it holds more than 1/1024 of
+# the launch's nonzeros -- i.e. when one wave walking it (~16 nonzeros in
+# flight) would outlast the rest of the launch.  Measured (scripts/
+# rank_work.py --sweep, Reddit shape): the full graph wants ~10 hubs (the
+# 1024-thread hub blocks otherwise queue behind the light rows: 988 hubs cost
+# +20%), a 1/8 row block wants its 132 rows above 2,048 as hubs (-25%).
+_HUB_ENV = os.environ.get("SGC_AMD_HUB_THRESHOLD")
+DEFAULT_HUB_THRESHOLD = int(_HUB_ENV) if _HUB_ENV else None
+HUB_SHARE = 1024
+
+
+def auto_hub_threshold(nnz_range, heavy_threshold):
+    return max(int(heavy_threshold), int(nnz_range) // HUB_SHARE)
 
 
 class Plan(NamedTuple):
@@ -132,6 +144,16 @@ class DeviceCSR:
         row_end = self.n_rows if row_end is None else row_end
         threshold = DEFAULT_HEAVY_THRESHOLD if threshold is None else int(threshold)
         hub = DEFAULT_HUB_THRESHOLD if hub_threshold is None else int(hub_threshold)
+        if hub is None:
+            auto = self._plans.get(("auto_hub", row_begin, row_end, threshold))
+            if auto is None:
+                nnz = 0
+                if row_end > row_begin:
+                    ends = self.row_ptr[[row_begin, row_end]].tolist()
+                    nnz = ends[1] - ends[0]
+                auto = auto_hub_threshold(nnz, threshold)
+                self._plans[("auto_hub", row_begin, row_end, threshold)] = auto
+            hub = auto
         hub = max(hub, threshold)
         key = (row_begin, row_end, threshold, hub)
         if key not in self._plans:

@@ -15,8 +15,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from sgc_amd.distributed import (RowPartitionedPropagator, equal_row_bounds, make_shard,
-                                 nnz_balanced_bounds)
+from sgc_amd.distributed import (FeaturePartitionedPropagator, RowPartitionedPropagator,
+                                 equal_row_bounds, feature_bounds, make_shard,
+                                 nnz_balanced_bounds, row_chunks)
 
 
 def _free_port():
@@ -50,7 +51,8 @@ def _oracle_spmm(shard, X, out):
     return out
 
 
-def _worker(rank, world, port, case, K, result_q, group_floats=128, staging=False):
+def _worker(rank, world, port, case, K, result_q, group_floats=128, staging=False,
+            output="replicated"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -61,22 +63,33 @@ def _worker(rank, world, port, case, K, result_q, group_floats=128, staging=Fals
         prop = RowPartitionedPropagator(shard, spmm_fn=_oracle_spmm, group_floats=group_floats,
                                         host_staging=staging)
         X0 = torch.from_numpy(case["X"])
-        out = prop.propagate(X0, K)
+        out = prop.propagate(X0, K, output=output)
         result_q.put((rank, out.numpy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,name,K,gf,staging", [
-    (2, "norm_n48_F65", 2, 128, False), (2, "hub1000_F65", 2, 16, False),
-    (3, "norm_n48_F602", 3, 128, False), (4, "raw_unsorted_dups_F7", 3, 2, False),
-    (2, "isolated_F17", 1, 4, True), (2, "norm_n48_F130", 2, 64, True)])
-def test_row_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, gf, staging):
+def _check_results(results, case, K, world, output, name):
+    want = case[f"Y{K}"]
+    rb = equal_row_bounds(want.shape[0], world)
+    for r in range(world):
+        w = want if output == "replicated" else want[rb[r]:rb[r + 1]]
+        assert results[r].shape == w.shape, (name, r)
+        assert np.array_equal(results[r].view(np.uint32), w.view(np.uint32)), (name, r)
+
+
+@pytest.mark.parametrize("world,name,K,gf,staging,output", [
+    (2, "norm_n48_F65", 2, 128, False, "replicated"), (2, "hub1000_F65", 2, 16, False, "sharded"),
+    (3, "norm_n48_F602", 3, 128, False, "replicated"), (3, "norm_n48_F602", 2, 128, False, "sharded"),
+    (4, "raw_unsorted_dups_F7", 3, 2, False, "replicated"),
+    (4, "raw_unsorted_dups_F7", 1, 2, False, "sharded"),
+    (2, "isolated_F17", 1, 4, True, "replicated"), (2, "norm_n48_F130", 2, 64, True, "sharded")])
+def test_row_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, gf, staging, output):
     case = tiny_cases[name]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, K, q, gf, staging))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, K, q, gf, staging, output))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -84,6 +97,151 @@ def test_row_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, gf, st
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    want = case[f"Y{K}"]
+    _check_results(results, case, K, world, output, name)
+
+
+# ---------------------------------------------------------------------------
+# Feature (column) partition: no exchange between hops, one chunked all-gather.
+
+def test_feature_bounds():
+    b, B = feature_bounds(602, 8)
+    assert B == 76 and b.tolist() == [0, 76, 152, 228, 304, 380, 456, 532, 602]
+    b, B = feature_bounds(602, 2)
+    assert B == 304 and b.tolist() == [0, 304, 602]
+    b, B = feature_bounds(5, 4)  # more ranks than aligned blocks: empty tails
+    assert B == 4 and b.tolist() == [0, 4, 5, 5, 5]
+    b, B = feature_bounds(7, 3, align=1)
+    assert B == 3 and b.tolist() == [0, 3, 6, 7]
+
+
+def test_row_chunks():
+    assert row_chunks(10, 4) == [(0, 3), (3, 6), (6, 9), (9, 10)]
+    assert row_chunks(3, 8) == [(0, 1), (1, 2), (2, 3)]
+    assert row_chunks(0, 4) == [(0, 0)]
+
+
+def _feature_worker(rank, world, port, case, K, result_q, chunks, align, staging, output):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as o
+        n = int(case["n"])
+        rp, ci, va = o.coo_to_csr(n, n, case["rows"], case["cols"], case["vals"])
+
+        def spmm_fn(X, r0, r1, out):
+            out.copy_(torch.from_numpy(o.spmm_csr(rp, ci, va, X.numpy(), r0, r1)))
+
+        prop = FeaturePartitionedPropagator(spmm_fn=spmm_fn, chunks=chunks, align=align,
+                                            host_staging=staging)
+        out = prop.propagate(torch.from_numpy(case["X"]), K, output=output)
+        out2 = prop.propagate(torch.from_numpy(case["X"]), K, output=output)  # buffers reused
+        assert torch.equal(out, out2)
+        result_q.put((rank, out.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name,K,chunks,align,staging,output", [
+    (2, "norm_n48_F602", 2, 4, 4, False, "replicated"), (2, "norm_n48_F602", 2, 4, 4, False, "sharded"),
+    (3, "norm_n48_F65", 3, 3, 4, False, "replicated"), (3, "norm_n48_F65", 2, 3, 4, False, "sharded"),
+    (4, "hub1000_F130", 2, 2, 4, False, "replicated"),
+    (4, "raw_unsorted_dups_F7", 3, 5, 1, False, "sharded"),
+    (2, "isolated_F17", 1, 1, 2, True, "replicated"), (3, "norm_n48_F3", 2, 4, 1, True, "sharded")])
+def test_feature_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, chunks, align,
+                                          staging, output):
+    case = tiny_cases[name]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_feature_worker,
+                         args=(r, world, port, case, K, q, chunks, align, staging, output))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _check_results(results, case, K, world, output, name)
+
+
+# ---------------------------------------------------------------------------
+# Data-parallel classifier over row shards (ShardedSGCTrainer).
+
+def _trainer_worker(rank, world, port, result_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sgc_amd.distributed import ShardedSGCTrainer, _torch_loss_grad
+        from sgc_amd.models import SGC
+        g = torch.Generator().manual_seed(0)
+        n, F, C = 97, 13, 5
+        X = torch.randn(n, F, generator=g)
+        y = torch.randint(0, C, (n,), generator=g)
+        train = torch.arange(0, n, 2)  # every other row trains
+        rb = equal_row_bounds(n, world)
+        r0, r1 = int(rb[rank]), int(rb[rank + 1])
+        mask = (train >= r0) & (train < r1)
+        Xl, yl = X[train[mask]], y[train[mask]]
+        torch.manual_seed(1)
+        model = SGC(F, C)
+        tr = ShardedSGCTrainer(model, loss_grad_fn=_torch_loss_grad)
+        loss0 = tr.loss(Xl, yl, train.numel())
+        g0 = (float(loss0), model.W.weight.grad.numpy().copy(), model.W.bias.grad.numpy().copy())
+        opt = torch.optim.LBFGS(model.parameters(), lr=1)
+
+        def closure():
+            opt.zero_grad()
+            return tr.loss(Xl, yl, train.numel())
+        for _ in range(2):
+            opt.step(closure)
+        result_q.put((rank, g0, model.W.weight.detach().numpy().copy(),
+                      model.W.bias.detach().numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_trainer_matches_single_process_lbfgs(world):
+    """reddit.py:51-64's LBFGS closure, data-parallel over row shards, ends at
+    the single-process weights (fp32 tolerance: the reduction order differs)."""
+    from sgc_amd.models import SGC
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict((r, (w, b, g0)) for r, g0, w, b in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = torch.Generator().manual_seed(0)
+    n, F, C = 97, 13, 5
+    X = torch.randn(n, F, generator=g)
+    y = torch.randint(0, C, (n,), generator=g)
+    train = torch.arange(0, n, 2)
+    torch.manual_seed(1)
+    model = SGC(F, C)
+    opt = torch.optim.LBFGS(model.parameters(), lr=1)
+
+    def closure():
+        opt.zero_grad()
+        z = X[train] @ model.W.weight.t() + model.W.bias
+        loss = torch.nn.functional.cross_entropy(z, y[train])
+        loss.backward()
+        return loss
+    loss0 = closure()
+    want0 = (float(loss0), model.W.weight.grad.numpy().copy(), model.W.bias.grad.numpy().copy())
+    for _ in range(2):
+        opt.step(closure)
     for r in range(world):
-        assert np.array_equal(results[r].view(np.uint32), want.view(np.uint32)), (name, r)
+        w, b, g0 = results[r]
+        # one closure: global mean loss and gradients (fp32 tolerance)
+        assert abs(g0[0] - want0[0]) <= 1e-6 * max(1.0, abs(want0[0]))
+        np.testing.assert_allclose(g0[1], want0[1], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(g0[2], want0[2], rtol=1e-5, atol=1e-6)
+        # two LBFGS steps (lr=1 amplifies rounding differences: looser)
+        np.testing.assert_allclose(w, model.W.weight.detach().numpy(), rtol=5e-3, atol=1e-4)
+        np.testing.assert_allclose(b, model.W.bias.detach().numpy(), rtol=5e-3, atol=1e-4)
+        assert np.array_equal(w, results[0][0])  # identical on every rank
