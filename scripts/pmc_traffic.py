@@ -107,13 +107,22 @@ def summarize(out_dir):
     hit, miss = _per_dispatch(l2, "TCC_HIT_sum"), _per_dispatch(l2, "TCC_MISS_sum")
 
     def spmm_dispatches(d):
+        """(calibration launches, Reddit-shape launches): main-kernel dispatch
+        ids, each Reddit launch paired with the hub-kernel dispatches of the
+        same sgc_spmm call (the hub rows' kernel runs beside the main one)."""
         ks = sorted(k for k, (nm, _, _) in d.items() if "spmm_csr_kernel" in nm)
-        return ks[:REPEATS], ks[REPEATS:2 * REPEATS]
+        hubs = sorted(k for k, (nm, _, _) in d.items() if "spmm_hub_kernel" in nm)
+        red = ks[REPEATS:2 * REPEATS]
+        return ks[:REPEATS], [[k] + [h for h in hubs if prev < h < k]
+                              for prev, k in zip([ks[REPEATS - 1]] + red[:-1], red)]
 
     cal_f, red_f = spmm_dispatches(fetch)
     cal_w, red_w = spmm_dispatches(write)
     cal_h, red_h = spmm_dispatches(hit)
-    mean = lambda d, ks: sum(d[k][2] for k in ks) / max(1, len(ks))  # noqa: E731
+
+    def mean(d, ks):  # ks: dispatch ids, or groups of ids summed per launch
+        vals = [sum(d[j][2] for j in k) if isinstance(k, list) else d[k][2] for k in ks]
+        return sum(vals) / max(1, len(vals))
     known_read = 4 * F_ * n_cal + 4 * (n_cal + 1) + 8 * n_cal
     known_write = 4 * F_ * n_cal
     cal_fetch_b = mean(fetch, cal_f) * 1024
