@@ -42,9 +42,11 @@ int sgc_abi_version(void);
 const char *sgc_last_error(void);
 
 /* Process-wide schedule knobs (results never depend on them).
- *   "slice_floats": feature-slice width of the SpMM grid (default 128;
+ *   "slice_floats": feature-slice width of the SpMM grid (default 0:
  *                   0 = one slice as wide as the registers allow);
- *   "max_vec":      widest per-lane load, 1, 2 or 4 floats (default 4).
+ *   "max_vec":      widest per-lane load, 1, 2 or 4 floats (default 4);
+ *   "hub_chunk":    features per hub-kernel workgroup, 32 or 64 (default 0 =
+ *                   32 when F <= 192 and X rows are 128-B aligned, else 64).
  * sgc_get_tuning returns -1 for an unknown key. */
 int sgc_set_tuning(const char *key, int64_t value);
 int64_t sgc_get_tuning(const char *key);
@@ -100,6 +102,30 @@ int sgc_augnorm_fill(const int32_t *row_ptr, const int32_t *col_idx, const doubl
                      int64_t n_rows, const double *d, int32_t *out_row_ptr,
                      int32_t *out_col_idx, float *out_val, void *workspace,
                      int64_t workspace_bytes, int64_t *out_nnz_host, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Induced sub-graph B = A[idx][:, idx] (reference utils.py:117, the inductive
+ * train sub-graph of reddit.py:44-47, taken on A + A^T before normalisation).
+ * A: CSR (int32), fp64 values; idx: int64 [m], distinct ids in [0, n_rows).
+ * B: canonical CSR (new row i = old row idx[i], new column = position in
+ * idx, ascending), fp64 values -- the input sgc_augnorm_count/fill take, so
+ * the S_train built from B is the reference's bit for bit.  Two synchronous
+ * calls around the host allocation of B, sharing one workspace:
+ *   sgc_subgraph_count: out_row_ptr [m+1], *out_nnz_host = nnz(B);
+ *     status_host bits: 1 = repeated ids (SGC_EINVAL), 2 = idx ascending,
+ *     4 = an id out of range (SGC_ERANGE);
+ *   sgc_subgraph_fill: out_col_idx / out_val [nnz(B)].
+ * workspace: sgc_subgraph_workspace(n_rows, m, nnz(A)) bytes.
+ * ------------------------------------------------------------------------- */
+int64_t sgc_subgraph_workspace(int64_t n_rows, int64_t m, int64_t nnz);
+int sgc_subgraph_count(const int32_t *row_ptr, const int32_t *col_idx, int64_t n_rows,
+                       int64_t nnz, const int64_t *idx, int64_t m, int32_t *out_row_ptr,
+                       void *workspace, int64_t workspace_bytes, int64_t *out_nnz_host,
+                       uint32_t *status_host, void *stream);
+int sgc_subgraph_fill(const int32_t *row_ptr, const int32_t *col_idx, const double *val,
+                      int64_t n_rows, int64_t nnz, const int64_t *idx, int64_t m,
+                      const int32_t *out_row_ptr, int32_t *out_col_idx, double *out_val,
+                      void *workspace, int64_t workspace_bytes, void *stream);
 
 /* CSR -> torch COO indices: rows64[k], cols64[k] (int64) of every entry. */
 int sgc_csr_to_coo64(const int32_t *row_ptr, const int32_t *col_idx, int64_t n_rows,

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--widths", default="128,224,602")
     ap.add_argument("--parts", default="1,8")
     ap.add_argument("--max-vec", default="4")
+    ap.add_argument("--hub-chunk", default="0")
+    ap.add_argument("--hubs", default="auto", help="hub thresholds per case ('auto' = default)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
@@ -47,17 +49,22 @@ def main():
         Xw[:, :w] = X[:, :w]
         for P in (int(x) for x in args.parts.split(",")):
             r0, r1 = 0, int(equal_row_bounds(S.n, P)[1])
-            pl = csr.plan(r0, r1)
             Y = torch.empty((r1 - r0, ld), device=dev)
             nz = int(rp[r1] - rp[r0])
             gb = (4 * (r1 - r0 + 1) + 8 * nz + 4 * w * nz + 4 * w * (r1 - r0)) / 1e9
-            cases.append((f"w{w}/P{P}", Xw, ld, w, r0, r1, pl, Y, gb))
+            for hb in args.hubs.split(","):
+                pl = csr.plan(r0, r1, None, None if hb == "auto" else int(hb))
+                cases.append((f"w{w}/P{P}/hub{hb}:{pl.n_hub}", Xw, ld, w, r0, r1, pl, Y, gb))
     mvs = [int(x) for x in args.max_vec.split(",")]
-    variants = [(name, lib, mv) for name, lib in loaded for mv in mvs]
+    hcs = [int(x) for x in args.hub_chunk.split(",")]
+    variants = [(f"{name}/hc{hc}", lib, (mv, hc)) for name, lib in loaded for mv in mvs
+                for hc in hcs]
 
-    def run(lib, mv, c):
+    def run(lib, cfg, c):
+        mv, hc = cfg
         _, Xw, ld, w, r0, r1, pl, Y, _ = c
         lib.sgc_set_tuning(b"max_vec", mv)
+        lib.sgc_set_tuning(b"hub_chunk", hc)
         rc = lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val),
                                   r0, r1, _lib.ptr(Xw), ld, _lib.ptr(Y), ld, w, _lib.ptr(pl.rows),
                                   pl.n_heavy, pl.n_hub, pl.threshold, stream)
@@ -73,7 +80,7 @@ def main():
             if ref is None:
                 ref = out
             elif not np.array_equal(ref, out):
-                raise SystemExit(f"variant {name} mv={mv} case {c[0]} is NOT bit-identical")
+                raise SystemExit(f"variant {name} cfg={mv} case {c[0]} is NOT bit-identical")
     times = {(c[0], v[0], v[2]): [] for c in cases for v in variants}
     for _ in range(args.rounds):
         for c in cases:
@@ -88,7 +95,7 @@ def main():
     gbs = {c[0]: c[8] for c in cases}
     for (case, name, mv), v in sorted(times.items()):
         med = float(np.median(v))
-        print(json.dumps({"case": case, "lib": name, "max_vec": mv, "median_ms": round(med, 4),
+        print(json.dumps({"case": case, "lib": name, "max_vec": mv[0], "median_ms": round(med, 4),
                           "gather_model_TBps": round(gbs[case] / med, 3)}), flush=True)
 
 

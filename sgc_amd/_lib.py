@@ -33,6 +33,11 @@ SIGNATURES = {
     "sgc_augnorm_fill": (ctypes.c_int, [_p, _p, _p, _i64, _p, _p, _p, _p, _p, _i64,
                                         ctypes.POINTER(_i64), _p]),
     "sgc_csr_to_coo64": (ctypes.c_int, [_p, _p, _i64, _p, _p, _p]),
+    "sgc_subgraph_workspace": (_i64, [_i64, _i64, _i64]),
+    "sgc_subgraph_count": (ctypes.c_int, [_p, _p, _i64, _i64, _p, _i64, _p, _p, _i64,
+                                          ctypes.POINTER(_i64), ctypes.POINTER(_u32), _p]),
+    "sgc_subgraph_fill": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _p, _p, _p, _i64,
+                                         _p]),
     "sgc_plan_capacity": (_i64, [_i64]),
     "sgc_plan_build": (ctypes.c_int, [_p, _i64, _i64, _i32, _i32, _p, _i64, ctypes.POINTER(_i64),
                                       ctypes.POINTER(_i64), _p]),

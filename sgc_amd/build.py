@@ -12,7 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsgc_amd.so")
-SOURCES = ["capi.hip", "spmm.hip", "ingest.hip", "linear.hip", "normalize.hip", "xent.hip"]
+SOURCES = ["capi.hip", "spmm.hip", "ingest.hip", "linear.hip", "normalize.hip", "xent.hip",
+           "subgraph.hip"]
 HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(ROOT, "include", "sgc_amd.h")]
 ARCH = os.environ.get("SGC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

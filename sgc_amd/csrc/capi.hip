@@ -46,6 +46,13 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
                     const int64_t *labels, int64_t M, int64_t K, int64_t C, float *loss,
                     float *dW, float *db, float *logits, int64_t ldl, void *ws, int64_t ws_bytes,
                     hipStream_t s);
+int64_t subgraph_workspace(int64_t n, int64_t m, int64_t nnz);
+int subgraph_count(const int32_t *row_ptr, const int32_t *col, int64_t n, const int64_t *idx,
+                   int64_t m, int64_t nnz, int32_t *out_row_ptr, void *ws, int64_t ws_bytes,
+                   int64_t *out_nnz_host, uint32_t *status_host, hipStream_t s);
+int subgraph_fill(const int32_t *row_ptr, const int32_t *col, const double *val, int64_t n,
+                  const int64_t *idx, int64_t m, int64_t nnz, const int32_t *out_row_ptr,
+                  int32_t *out_col, double *out_val, void *ws, int64_t ws_bytes, hipStream_t s);
 int set_tuning(const char *key, int64_t value);
 int64_t get_tuning(const char *key);
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
@@ -107,6 +114,26 @@ int sgc_augnorm_fill(const int32_t *row_ptr, const int32_t *col_idx, const doubl
     return augnorm_fill(row_ptr, col_idx, val, n_rows, d, out_row_ptr, out_col_idx, out_val,
                         workspace, workspace_bytes < 0 ? 0 : (size_t)workspace_bytes,
                         out_nnz_host, as_stream(stream));
+}
+
+int64_t sgc_subgraph_workspace(int64_t n_rows, int64_t m, int64_t nnz) {
+    return subgraph_workspace(n_rows, m, nnz);
+}
+
+int sgc_subgraph_count(const int32_t *row_ptr, const int32_t *col_idx, int64_t n_rows,
+                       int64_t nnz, const int64_t *idx, int64_t m, int32_t *out_row_ptr,
+                       void *workspace, int64_t workspace_bytes, int64_t *out_nnz_host,
+                       uint32_t *status_host, void *stream) {
+    return subgraph_count(row_ptr, col_idx, n_rows, idx, m, nnz, out_row_ptr, workspace,
+                          workspace_bytes, out_nnz_host, status_host, as_stream(stream));
+}
+
+int sgc_subgraph_fill(const int32_t *row_ptr, const int32_t *col_idx, const double *val,
+                      int64_t n_rows, int64_t nnz, const int64_t *idx, int64_t m,
+                      const int32_t *out_row_ptr, int32_t *out_col_idx, double *out_val,
+                      void *workspace, int64_t workspace_bytes, void *stream) {
+    return subgraph_fill(row_ptr, col_idx, val, n_rows, idx, m, nnz, out_row_ptr, out_col_idx,
+                         out_val, workspace, workspace_bytes, as_stream(stream));
 }
 
 int sgc_csr_to_coo64(const int32_t *row_ptr, const int32_t *col_idx, int64_t n_rows,

@@ -172,72 +172,118 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 
 // ---------------------------------------------------------------------------
 // Hub rows (degree > hub_threshold): one 1024-thread workgroup per (row,
-// 64-feature chunk).  A single wave's FMA chain over d nonzeros costs d FMAs
+// HC-feature chunk).  A single wave's FMA chain over d nonzeros costs d FMAs
 // -- cheap -- but a wave keeps only ~16 nonzeros' X segments in flight, so a
 // 48k-nonzero hub on one wave runs ~3 ms, longer than a whole hop at P >= 2
-// GPUs.  Here 15 loader waves gather the next 240 nonzeros' 256-B X segments
-// (registers -> LDS, double buffered) while wave 0 runs the sequential
-// chain out of LDS: ~60 KB in flight per hub chunk, the same FMA order.
-constexpr int kHubChunk = 64;
+// GPUs.  Here 15 loader waves gather X segments into an LDS double buffer
+// while wave 0 runs the sequential chain out of LDS -- the same FMA order.
+//
+// The chain is the block's floor, so:
+//  * wave 0 reads four nonzeros' X values per lane with one ds_read_b128 and
+//    their four values with one broadcast ds_read_b128: the staging image is
+//    transposed, gxT[feature][nonzero], row stride kStride = 4 mod 64 dwords
+//    (conflict-free b128 reads per 16-lane group and b128 writes per 8-lane
+//    group); each loader lane holds 16 CONSECUTIVE nonzeros of its feature
+//    and writes them with four ds_write_b128;
+//  * loaders keep kHubDepth rounds in registers: round t+kHubDepth is issued
+//    while round t+1 is written, so a load has kHubDepth-1 rounds of FMA time
+//    to land (a round is ~0.5 us of chain; an HBM/IC gather ~1-2 us).
+// HC = 32 (one 128-B line per nonzero; lanes 32-63 load the second 16
+// nonzeros of the loader's run) halves the bytes each block ingests per
+// nonzero and spreads a hub over twice the CUs; it needs 128-B aligned X rows
+// to stay one line per segment.
 constexpr int kHubLoaders = 15;
-constexpr int kHubPerLoader = 16;
-constexpr int kHubRound = kHubLoaders * kHubPerLoader;  // 240 nonzeros per round
+constexpr int kHubInstr = 16;  // consecutive nonzeros per loader lane per round
+constexpr int kHubDepth = 3;   // rounds held in loader registers
 
+template <int HC>
+struct HubShape {
+    static constexpr int kSegs = kWave / HC;                     // nonzero runs per loader wave
+    static constexpr int kPerLoader = kHubInstr * kSegs;         // nonzeros per loader per round
+    static constexpr int kRound = kHubLoaders * kPerLoader;      // nonzeros per round (240 / 480)
+    static constexpr int kStride = (kRound + 63) / 64 * 64 + 4;  // dwords per gxT row (4 mod 64)
+};
+
+template <int HC>
 __global__ __launch_bounds__(1024) void spmm_hub_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy, int row_begin,
     int F, const int *__restrict__ hub_rows, int n_chunks) {
-    __shared__ float gx[2][kHubRound][kHubChunk];  // 120 KB
-    __shared__ float gv[2][kHubRound];
+    using Sh = HubShape<HC>;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) float gxT[2][HC * Sh::kStride];  // 2 x 66.5 KB
+    __shared__ __attribute__((aligned(16))) float gv[2][Sh::kRound];
     const int lane = threadIdx.x & (kWave - 1);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
     const int h = blockIdx.x / n_chunks;
     const int c = blockIdx.x - h * n_chunks;
     const int row = hub_rows[h];
     const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
-    const int f = c * kHubChunk + lane;
+    const int fl = lane & (HC - 1);  // feature within the chunk
+    const int seg = lane / HC;       // which run of kHubInstr nonzeros (HC = 32: 0 or 1)
+    const int f = c * HC + fl;
     const uint32_t boff = (f < F ? (uint32_t)f : 0u) * 4u;
     const char *Xb = reinterpret_cast<const char *>(X);
     const int64_t row_bytes = ldx * 4;
-    const int n_round = (k1 - k0 + kHubRound - 1) / kHubRound;
-    float regs[kHubPerLoader];
-    float vreg = 0.f;
-    auto load = [&](int r) {  // loader waves only; wave-uniform k
-        const int kb = k0 + r * kHubRound + (w - 1) * kHubPerLoader;
+    const int n_round = (k1 - k0 + Sh::kRound - 1) / Sh::kRound;
+    float regs[kHubDepth][kHubInstr];
+    float vreg[kHubDepth];
+    // loader waves only; `s` is always a compile-time constant after unrolling
+    auto load = [&](int r, int s) {
+        const int kr = k0 + r * Sh::kRound + (w - 1) * Sh::kPerLoader;
+        const int kb = kr + seg * kHubInstr;
 #pragma unroll
-        for (int j = 0; j < kHubPerLoader; ++j) {
-            const int k = min(kb + j, k1 - 1);
-            const int cj = col[k];
-            regs[j] = *reinterpret_cast<const float *>(Xb + (int64_t)cj * row_bytes + boff);
+        for (int j = 0; j < kHubInstr; ++j) {
+            const int cj = col[min(kb + j, k1 - 1)];
+            regs[s][j] = *reinterpret_cast<const float *>(Xb + (int64_t)cj * row_bytes + boff);
         }
-        const int kl = min(kb + (lane & (kHubPerLoader - 1)), k1 - 1);
-        vreg = val[kl];
+        vreg[s] = val[min(kr + (lane & (Sh::kPerLoader - 1)), k1 - 1)];
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, int s) {
+        f4 *dst = reinterpret_cast<f4 *>(
+            &gxT[buf][fl * Sh::kStride + (w - 1) * Sh::kPerLoader + seg * kHubInstr]);
 #pragma unroll
-        for (int j = 0; j < kHubPerLoader; ++j) gx[buf][(w - 1) * kHubPerLoader + j][lane] = regs[j];
-        if (lane < kHubPerLoader) gv[buf][(w - 1) * kHubPerLoader + lane] = vreg;
+        for (int q = 0; q < kHubInstr / 4; ++q)
+            dst[q] = f4{regs[s][4 * q], regs[s][4 * q + 1], regs[s][4 * q + 2], regs[s][4 * q + 3]};
+        if (lane < Sh::kPerLoader) gv[buf][(w - 1) * Sh::kPerLoader + lane] = vreg[s];
     };
-    if (w > 0 && n_round > 0) {
-        load(0);
-        store(0);
+    if (w > 0) {
+#pragma unroll
+        for (int s = 0; s < kHubDepth; ++s)
+            if (s < n_round) load(s, s);
+        if (n_round > 0) store(0, 0);
     }
     __syncthreads();
     float acc = 0.0f;
-    for (int r = 0; r < n_round; ++r) {
-        const int buf = r & 1;
-        if (w > 0) {
-            if (r + 1 < n_round) {
-                load(r + 1);
-                store(buf ^ 1);
+    for (int r0 = 0; r0 < n_round; r0 += kHubDepth) {
+#pragma unroll
+        for (int s = 0; s < kHubDepth; ++s) {
+            const int r = r0 + s;  // round t lives in regs[t % kHubDepth]
+            if (r >= n_round) break;  // block-uniform
+            const int buf = r & 1;
+            if (w > 0) {
+                if (r + 1 < n_round) store(buf ^ 1, (s + 1) % kHubDepth);
+                if (r + kHubDepth < n_round) load(r + kHubDepth, s);
+            } else {
+                const int n = min(Sh::kRound, k1 - (k0 + r * Sh::kRound));
+                const f4 *xs = reinterpret_cast<const f4 *>(&gxT[buf][fl * Sh::kStride]);
+                const f4 *vs = reinterpret_cast<const f4 *>(&gv[buf][0]);
+                const int n4 = n >> 2;
+#pragma unroll 4
+                for (int q = 0; q < n4; ++q) {
+                    const f4 x = xs[q], v = vs[q];
+                    acc = __builtin_fmaf(v[0], x[0], acc);
+                    acc = __builtin_fmaf(v[1], x[1], acc);
+                    acc = __builtin_fmaf(v[2], x[2], acc);
+                    acc = __builtin_fmaf(v[3], x[3], acc);
+                }
+                const float *xt = &gxT[buf][fl * Sh::kStride];
+                for (int kk = n4 * 4; kk < n; ++kk) acc = __builtin_fmaf(gv[buf][kk], xt[kk], acc);
             }
-        } else {
-            const int n = min(kHubRound, k1 - (k0 + r * kHubRound));
-            for (int kk = 0; kk < n; ++kk) acc = __builtin_fmaf(gv[buf][kk], gx[buf][kk][lane], acc);
+            __syncthreads();
         }
-        __syncthreads();
     }
-    if (w == 0 && f < F) Y[(int64_t)(row - row_begin) * ldy + f] = acc;
+    if (w == 0 && seg == 0 && f < F) Y[(int64_t)(row - row_begin) * ldy + f] = acc;
 }
 
 namespace {
@@ -338,12 +384,20 @@ constexpr int max_chunks(int V) { return 16 / V; }  // <= 16 accumulators per la
 // Slice width in 64V-float chunks; 0 = widest the registers allow (one
 // slice for F <= 64*16).  Set through sgc_set_tuning("slice_floats", n).
 static int g_slice_floats = 0;
+// Hub-kernel feature chunk: 0 = auto (32 on 128-B aligned X rows, else 64).
+static int g_hub_chunk = 0;
 
 int set_tuning(const char *key, int64_t value) {
     SGC_REQUIRE(key, SGC_EINVAL, "set_tuning: null key");
     if (std::string(key) == "slice_floats") {
         SGC_REQUIRE(value >= 0 && value < (1 << 20), SGC_EINVAL, "slice_floats out of range");
         g_slice_floats = (int)value;
+        return SGC_OK;
+    }
+    if (std::string(key) == "hub_chunk") {
+        SGC_REQUIRE(value == 0 || value == 32 || value == 64, SGC_EINVAL,
+                    "hub_chunk must be 0 (auto), 32 or 64");
+        g_hub_chunk = (int)value;
         return SGC_OK;
     }
     if (std::string(key) == "max_vec") {
@@ -358,6 +412,7 @@ int set_tuning(const char *key, int64_t value) {
 int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "slice_floats") return g_slice_floats;
     if (key && std::string(key) == "max_vec") return g_max_vec;
+    if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
     return -1;
 }
 
@@ -382,14 +437,24 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     SideStream *side = nullptr;
     if (n_hub > 0) {
         // hub rows (the heaviest n_hub of the plan) run on the side stream
-        const int n_chunks = (int)((F + kHubChunk - 1) / kHubChunk);
+        // 32-feature chunks spread a hub over more CUs; measured faster up to
+        // F = 160 and slower from F = 320 (scripts/sweep_narrow.py), and they
+        // need 128-B aligned rows to stay one line per segment.
+        const bool lines = ldx % 32 == 0 && reinterpret_cast<uintptr_t>(X) % 128 == 0;
+        const int hc = g_hub_chunk ? g_hub_chunk : (lines && F <= 192 ? 32 : 64);
+        const int n_chunks = (int)((F + hc - 1) / hc);
         SGC_REQUIRE(n_hub * n_chunks < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many hub items");
         SGC_HIP_CHECK(side_stream(&side));
         SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
         SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
-        hipLaunchKernelGGL(spmm_hub_kernel, dim3((unsigned)(n_hub * n_chunks)), dim3(1024), 0,
-                           side->s, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)F,
-                           heavy_rows, n_chunks);
+        if (hc == 32)
+            hipLaunchKernelGGL(spmm_hub_kernel<32>, dim3((unsigned)(n_hub * n_chunks)), dim3(1024),
+                               0, side->s, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
+                               (int)F, heavy_rows, n_chunks);
+        else
+            hipLaunchKernelGGL(spmm_hub_kernel<64>, dim3((unsigned)(n_hub * n_chunks)), dim3(1024),
+                               0, side->s, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
+                               (int)F, heavy_rows, n_chunks);
         SGC_HIP_CHECK(hipGetLastError());
         heavy_rows += n_hub;
         n_heavy -= n_hub;

@@ -61,24 +61,76 @@ def aug_normalize_on_device(adj, device="cuda"):
     columns), which is what the loaders produce (networkx adjacency, A + A^T).
     The only host step is the one the reference itself does in numpy:
     d = rowsum ** -0.5 with inf -> 0 (normalization.py:8-10)."""
+    return aug_normalize_device_arrays(*device_csr64(adj, device))
+
+
+def device_csr64(adj, device="cuda"):
+    """Canonical scipy CSR A -> (row_ptr int32, col_idx int32, val fp64, n)
+    on the device: the input of the on-device AugNorm and sub-graph kernels."""
+    import torch
+    a = sp.csr_matrix(adj)
+    if not a.has_canonical_format:
+        raise ValueError("sgc_amd: A must be canonical CSR (sorted unique column indices); "
+                         "use aug_normalized_adjacency")
+    if a.shape[0] != a.shape[1]:
+        raise ValueError("sgc_amd: A must be square")
+    n = a.shape[0]
+    if n >= 2**31 - 1 or a.nnz >= 2**31 - 1:
+        raise ValueError("sgc_amd: beyond int32 CSR")
+    dev = torch.device(device)
+    rp = torch.from_numpy(a.indptr.astype(np.int32)).to(dev)
+    ci = torch.from_numpy(a.indices.astype(np.int32)).to(dev)
+    va = torch.from_numpy(a.data.astype(np.float64)).to(dev)
+    return rp, ci, va, n
+
+
+def subgraph_on_device(rp, ci, va, n, idx):
+    """B = A[idx][:, idx] on the device (reference utils.py:117, the inductive
+    train sub-graph), from device_csr64 arrays: canonical CSR with fp64 values
+    (new row i = old row idx[i], new column = position in idx), ready for
+    aug_normalize_device_arrays -- whose S is then the reference's
+    fetch_normalization('AugNormAdj')(adj[idx, :][:, idx]) bit for bit.
+    Repeated ids raise ValueError (the host slice handles them)."""
+    import torch
+
+    from . import _lib
+    from .propagate import ctypes_byref
+    dev = rp.device
+    idx_t = torch.as_tensor(np.asarray(idx, dtype=np.int64)).to(dev)
+    m, nnz = int(idx_t.numel()), int(ci.numel())
+    lib = _lib.load()
+    ws_bytes = lib.sgc_subgraph_workspace(n, m, nnz)
+    ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8, device=dev)
+    out_rp = torch.empty(m + 1, dtype=torch.int32, device=dev)
+    total, status = _lib._i64(0), _lib._u32(0)
+    with torch.cuda.device(dev):
+        stream = _lib.stream_handle(dev)
+        rc = lib.sgc_subgraph_count(_lib.ptr(rp), _lib.ptr(ci), n, nnz, _lib.ptr(idx_t), m,
+                                    _lib.ptr(out_rp), _lib.ptr(ws), ws_bytes, ctypes_byref(total),
+                                    ctypes_byref(status), stream)
+        if rc == 1 and status.value & 1:
+            raise ValueError("subgraph_on_device: repeated indices")
+        _lib.check(rc, "subgraph_count")
+        t = int(total.value)
+        out_ci = torch.empty(max(t, 1), dtype=torch.int32, device=dev)
+        out_va = torch.empty(max(t, 1), dtype=torch.float64, device=dev)
+        _lib.check(lib.sgc_subgraph_fill(_lib.ptr(rp), _lib.ptr(ci), _lib.ptr(va), n, nnz,
+                                         _lib.ptr(idx_t), m, _lib.ptr(out_rp), _lib.ptr(out_ci),
+                                         _lib.ptr(out_va), _lib.ptr(ws), ws_bytes, stream),
+                   "subgraph_fill")
+    return out_rp, out_ci[:t], out_va[:t], m
+
+
+def aug_normalize_device_arrays(rp, ci, va, n):
+    """S = AugNorm(A) on the device from canonical CSR arrays (device_csr64 /
+    subgraph_on_device); see aug_normalize_on_device."""
     import torch
 
     from . import _lib
     from .propagate import DeviceCSR, ctypes_byref
-    a = sp.csr_matrix(adj)
-    if not a.has_canonical_format:
-        raise ValueError("aug_normalize_on_device: A must be canonical CSR "
-                         "(sorted unique column indices); use aug_normalized_adjacency")
-    n = a.shape[0]
-    if a.shape[0] != a.shape[1]:
-        raise ValueError("aug_normalize_on_device: A must be square")
-    if n >= 2**31 - 1 or a.nnz >= 2**31 - 1:
-        raise ValueError("aug_normalize_on_device: beyond int32 CSR")
-    dev = torch.device(device)
+    dev = rp.device
+    a_nnz = int(ci.numel())
     lib = _lib.load()
-    rp = torch.from_numpy(a.indptr.astype(np.int32)).to(dev)
-    ci = torch.from_numpy(a.indices.astype(np.int32)).to(dev)
-    va = torch.from_numpy(a.data.astype(np.float64)).to(dev)
     out_rp = torch.empty(n + 1, dtype=torch.int32, device=dev)
     rowsum = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
     ws_bytes = lib.sgc_augnorm_workspace(n)
@@ -86,7 +138,7 @@ def aug_normalize_on_device(adj, device="cuda"):
     nnz_out, status = _lib._i64(0), _lib._u32(0)
     with torch.cuda.device(dev):
         stream = _lib.stream_handle(dev)
-        _lib.check(lib.sgc_augnorm_count(_lib.ptr(rp), _lib.ptr(ci), _lib.ptr(va), n, a.nnz,
+        _lib.check(lib.sgc_augnorm_count(_lib.ptr(rp), _lib.ptr(ci), _lib.ptr(va), n, a_nnz,
                                          _lib.ptr(out_rp), _lib.ptr(rowsum), _lib.ptr(ws), ws_bytes,
                                          ctypes_byref(nnz_out), ctypes_byref(status), stream),
                    "augnorm_count")

@@ -54,6 +54,25 @@ def _normalized_adj(adj, normalization, cuda):
     return t.cuda() if cuda else t
 
 
+def _reddit_adjs(adj, train_index, normalization, cuda):
+    """(S, S_train) for load_reddit_data (reference utils.py:116-124): the
+    train sub-graph is sliced from A + A^T BEFORE normalisation.  On the GPU
+    (canonical A, 'AugNormAdj', distinct train ids) A is uploaded once and both
+    the slice (sgc_subgraph_*) and both normalisations run on the device --
+    bit-identical to the reference's scipy path; otherwise the host path."""
+    a = sp.csr_matrix(adj)
+    idx = np.asarray(train_index, dtype=np.int64)
+    if (cuda and normalization == "AugNormAdj" and a.has_canonical_format
+            and np.unique(idx).size == idx.size):
+        from .normalization import aug_normalize_device_arrays, device_csr64, subgraph_on_device
+        rp, ci, va, n = device_csr64(a, "cuda")
+        full = to_torch_coo(aug_normalize_device_arrays(rp, ci, va, n))
+        sub = to_torch_coo(aug_normalize_device_arrays(*subgraph_on_device(rp, ci, va, n, idx)))
+        return full, sub
+    return (_normalized_adj(adj, normalization, cuda),
+            _normalized_adj(adj[idx, :][:, idx], normalization, cuda))
+
+
 def sgc_precompute(features, adj, degree):
     """X_K = S^K X on the GPU; returns (features_K, seconds) like utils.py:92-97.
 
@@ -157,11 +176,9 @@ def load_reddit_data(data_path="data/", normalization="AugNormAdj", cuda=True):
     labels[val_index] = y_val
     labels[test_index] = y_test
     adj = adj + adj.T
-    train_adj = adj[train_index, :][:, train_index]
     features = torch.FloatTensor(np.array(features))
     features = (features - features.mean(dim=0)) / features.std(dim=0)
-    adj = _normalized_adj(adj, normalization, cuda)
-    train_adj = _normalized_adj(train_adj, normalization, cuda)
+    adj, train_adj = _reddit_adjs(adj, train_index, normalization, cuda)
     labels = torch.LongTensor(labels)
     if cuda:
         features, labels = features.cuda(), labels.cuda()

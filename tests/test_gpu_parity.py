@@ -54,10 +54,23 @@ def test_tiny_cases_sgc_precompute_bit_exact(tiny_cases):
             assert bits_equal(out.cpu().numpy(), c[key]), (name, K)
 
 
+@pytest.mark.parametrize("hub_chunk", [0, 32, 64])
 @pytest.mark.parametrize("threshold,hub", [(0, 0), (1, 7), (7, 7), (63, 500), (0, 10**9),
                                            (10**9, 10**9), (2048, 4096)])
-def test_heavy_split_schedule_never_changes_bits(tiny_cases, threshold, hub):
-    """Every row a hub (0, 0), every row heavy (0, inf) .. no heavy rows: same bits."""
+def test_heavy_split_schedule_never_changes_bits(tiny_cases, threshold, hub, hub_chunk):
+    """Every row a hub (0, 0), every row heavy (0, inf) .. no heavy rows, hub
+    kernel on 32- or 64-feature chunks: same bits."""
+    from sgc_amd import _lib
+    from sgc_amd.propagate import DeviceCSR, propagate
+    lib = _lib.load()
+    _lib.check(lib.sgc_set_tuning(b"hub_chunk", hub_chunk), "set_tuning")
+    try:
+        _schedule_cases(tiny_cases, threshold, hub)
+    finally:
+        lib.sgc_set_tuning(b"hub_chunk", 0)
+
+
+def _schedule_cases(tiny_cases, threshold, hub):
     from sgc_amd.propagate import DeviceCSR, propagate
     for name in ("hub1000_F65", "hub1000_F130", "norm_n48_F602", "norm_n48_F130",
                  "norm_n48_F3", "raw_sorted_dups_F66", "raw_unsorted_dups_F7", "special_values_F11",
