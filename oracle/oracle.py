@@ -106,3 +106,27 @@ def linear(X, W, b):
     bp = _ptr(np.ascontiguousarray(b, dtype=np.float32)) if b is not None else None
     _check(lib().oracle_linear_f64acc(M, K, C, _ptr(X), _ptr(W), bp, _ptr(Y)), "linear")
     return Y
+
+
+def textsgc_precompute(row_ptr, col_idx, val, dense, index_dict):
+    """TextSGC's one-hop precompute restated (reference
+    downstream/TextSGC/utils.py:131-152) on the oracle SpMM:
+    for each split, F = (S . dense[:, idx])^T; train fixes the columns with a
+    positive range over the training rows and their min/range; every split is
+    (F[:, useful] - min) / range.  Returns {split: float32 array}."""
+    import numpy as _np
+    out = {}
+
+    def hop(idx):
+        X = _np.ascontiguousarray(dense[:, _np.asarray(idx)], dtype=_np.float32)
+        return _np.ascontiguousarray(spmm_csr(row_ptr, col_idx, val, X).T)
+
+    tr = hop(index_dict["train"])
+    mx, mn = tr.max(axis=0, keepdims=True), tr.min(axis=0, keepdims=True)
+    rng = mx - mn
+    useful = _np.nonzero(rng.squeeze(0) > 0)[0]
+    mn, rng = mn[:, useful], rng[:, useful]
+    out["train"] = (tr[:, useful] - mn) / rng
+    for phase in ("test", "val"):
+        out[phase] = (hop(index_dict[phase])[:, useful] - mn) / rng
+    return out

@@ -5,6 +5,7 @@ tiny case and every shape hash in tests/golden/ was produced by the
 reference's own sgc_precompute (torch.spmm on CPU) in the build container.
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -77,3 +78,20 @@ def test_oracle_linear_matches_torch_fp32():
     Y = o.linear(X, W, b)
     ref = torch.nn.functional.linear(torch.from_numpy(X), torch.from_numpy(W), torch.from_numpy(b))
     np.testing.assert_allclose(Y, ref.numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_textsgc_oracle_matches_reference_golden(oracle):
+    """The TextSGC restatement (oracle.textsgc_precompute) against the
+    reference's own function's outputs (tests/golden/gen_textsgc.py)."""
+    import scipy.sparse as sp
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "textsgc_case.npz"))
+    n = int(z["n"])
+    S = sp.csr_matrix((z["data"], z["indices"], z["indptr"]), shape=(n, n))
+    coo = S.tocoo().astype(np.float32)
+    rp, ci, va = oracle.coo_to_csr(n, n, coo.row, coo.col, coo.data)
+    dense = np.asarray(S.todense()).astype(np.float32)
+    idx = {k: z[f"idx_{k}"] for k in ("train", "val", "test")}
+    got = oracle.textsgc_precompute(rp, ci, va, dense, idx)
+    for k in ("train", "val", "test"):
+        assert got[k].shape == z[f"feat_{k}"].shape, k
+        assert np.array_equal(got[k].view(np.uint32), z[f"feat_{k}"].view(np.uint32)), k
