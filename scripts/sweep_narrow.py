@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--max-vec", default="4")
     ap.add_argument("--hub-chunk", default="0")
     ap.add_argument("--hubs", default="auto", help="hub thresholds per case ('auto' = default)")
+    ap.add_argument("--unaligned", action="store_true",
+                    help="also read each width straight from the [N, 602] input (ld 602)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
@@ -55,6 +57,9 @@ def main():
             for hb in args.hubs.split(","):
                 pl = csr.plan(r0, r1, None, None if hb == "auto" else int(hb))
                 cases.append((f"w{w}/P{P}/hub{hb}:{pl.n_hub}", Xw, ld, w, r0, r1, pl, Y, gb))
+                if args.unaligned:
+                    cases.append((f"w{w}/P{P}/hub{hb}:{pl.n_hub}/ld602", X, F, w, r0, r1, pl, Y,
+                                  gb))
     mvs = [int(x) for x in args.max_vec.split(",")]
     hcs = [int(x) for x in args.hub_chunk.split(",")]
     variants = [(f"{name}/hc{hc}", lib, (mv, hc)) for name, lib in loaded for mv in mvs
@@ -66,7 +71,8 @@ def main():
         lib.sgc_set_tuning(b"max_vec", mv)
         lib.sgc_set_tuning(b"hub_chunk", hc)
         rc = lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val),
-                                  r0, r1, _lib.ptr(Xw), ld, _lib.ptr(Y), ld, w, _lib.ptr(pl.rows),
+                                  r0, r1, _lib.ptr(Xw), ld, _lib.ptr(Y), Y.stride(0), w,
+                                  _lib.ptr(pl.rows),
                                   pl.n_heavy, pl.n_hub, pl.threshold, stream)
         if rc:
             raise RuntimeError(lib.sgc_last_error())

@@ -125,8 +125,14 @@ class RowPartitionedPropagator:
     columns are computed and never returned)."""
 
     def __init__(self, shard: ShardCSR, group=None, spmm_fn: Optional[Callable] = None,
-                 group_floats: int = 320, host_staging: bool = False):
+                 group_floats: int = 320, host_staging: bool = False,
+                 pad_input: Optional[bool] = None):
         self.shard = shard
+        # Re-lay X_0 into 128-B rows before hop 1?  The copy (all N rows, ~0.2 ms
+        # at Reddit shape) beats reading 8-B aligned rows only while this rank's
+        # hop-1 share is large: unaligned reads cost +10-18% of that hop
+        # (profiles/r01_unaligned_input_sweep.log), so None = pad up to P = 4.
+        self.pad_input = pad_input
         self.group = group
         self.spmm_fn = spmm_fn or _default_spmm
         self.group_floats = max(2, int(group_floats) // 2 * 2)  # 8-B aligned groups
@@ -165,14 +171,16 @@ class RowPartitionedPropagator:
         if X0.is_cuda:
             from . import _lib
             from .propagate import aligned_ld
-            Fp = aligned_ld(F)
-            Xa = self._buf("x0", (n, Fp), X0)  # 128-B rows (propagate() does the same)
-            _lib.check(_lib.load().sgc_pad_rows_f32(
-                _lib.ptr(X0), X0.stride(0), _lib.ptr(Xa), Fp, n, F,
-                _lib.stream_handle(X0.device)), "pad_rows_f32")
-            X0 = Xa
+            Fp = aligned_ld(F)  # exchanged buffers keep 128-B rows either way
+            pad = self.pad_input if self.pad_input is not None else s.world_size <= 4
+            if pad:
+                Xa = self._buf("x0", (n, Fp), X0)  # 128-B rows (propagate() does the same)
+                _lib.check(_lib.load().sgc_pad_rows_f32(
+                    _lib.ptr(X0), X0.stride(0), _lib.ptr(Xa), Fp, n, F,
+                    _lib.stream_handle(X0.device)), "pad_rows_f32")
+                X0 = Xa
         groups = [(a, min(Fp, a + self.group_floats)) for a in range(0, Fp, self.group_floats)]
-        src = [X0[:, a:b] for a, b in groups]
+        src = [X0[:, a:min(b, X0.shape[1])] for a, b in groups]  # unpadded: last one narrower
         works = [None] * len(groups)
         if output == "sharded":
             K_ex = K - 1  # hops whose output is exchanged
@@ -188,7 +196,7 @@ class RowPartitionedPropagator:
                     works[gi].wait()  # this hop's input group has arrived (stream wait)
                 loc = self._buf(("local", par, gi), (s.block, b - a), X0)
                 if s.rows:
-                    self.spmm_fn(s, src[gi], loc[:s.rows])
+                    self.spmm_fn(s, src[gi], loc[:s.rows, :src[gi].shape[1]])
                 full = self._buf(("full", par, gi), (s.world_size * s.block, b - a), X0)
                 new_works.append(self._all_gather(full, loc))
                 gathered.append(full)

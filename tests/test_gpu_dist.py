@@ -29,16 +29,22 @@ def nccl_group():
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("pad_input", [None, False])
 @pytest.mark.parametrize("output", ["replicated", "sharded"])
 @pytest.mark.parametrize("name,K,gf", [("norm_n48_F602", 2, 128), ("hub1000_F130", 2, 64),
-                                       ("norm_n48_F65", 3, 32), ("isolated_F17", 1, 128)])
-def test_rccl_row_partition_bit_exact(nccl_group, tiny_cases, oracle, name, K, gf, output):
+                                       ("norm_n48_F65", 3, 32), ("isolated_F17", 1, 128),
+                                       ("norm_n48_F602", 3, 320)])
+def test_rccl_row_partition_bit_exact(nccl_group, tiny_cases, oracle, name, K, gf, output,
+                                      pad_input):
+    """pad_input=False: hop 1 reads the caller's 8-B aligned rows directly and
+    the last feature group is narrower than its exchange buffer (the P >= 8
+    default)."""
     from sgc_amd.distributed import RowPartitionedPropagator, make_shard
     c = tiny_cases[name]
     n = int(c["n"])
     rp, ci, va = oracle.coo_to_csr(n, n, c["rows"], c["cols"], c["vals"])
     shard = make_shard(rp, ci, va, 0, 1, "cuda")
-    prop = RowPartitionedPropagator(shard, group_floats=gf)
+    prop = RowPartitionedPropagator(shard, group_floats=gf, pad_input=pad_input)
     out = prop.propagate(torch.from_numpy(c["X"]).cuda(), K, output=output)
     torch.cuda.synchronize()
     want = c[f"Y{K}"]
