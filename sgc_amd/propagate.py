@@ -309,6 +309,52 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
     return out
 
 
+class GraphedPropagation:
+    """The K-hop loop of propagate() captured once into a HIP graph, for
+    repeated propagation over one adjacency at one feature shape (many feature
+    sets, serving, hyper-parameter sweeps like the reference's tuning.py).
+
+    It makes the whole loop -- pad copy, K SpMM launches, the hub kernels'
+    fork/join on the side stream -- one replayable unit, e.g. inside a larger
+    captured serving step.  It is not a speed-up on its own: even at Pubmed
+    shape a hop is GPU-bound (~70 us of kernel time), and a replay measured
+    191 us against 163 us eager, the static-input copy included
+    (profiles/r01_bench_small.log).  run(X) copies X into the graph's static
+    input and replays; the result is in self.out (bit-identical to
+    propagate()).
+    Capture builds the plan first (it synchronises) and warms the code
+    objects on a side stream, as torch.cuda.graph requires."""
+
+    def __init__(self, csr: DeviceCSR, shape, K: int, threshold=None, hub_threshold=None):
+        n, F = shape
+        if K < 1:
+            raise ValueError("GraphedPropagation: K >= 1")
+        self.csr, self.K = csr, int(K)
+        self.x_in = torch.empty((n, F), dtype=torch.float32, device=csr.device)
+        self.out = torch.empty((n, F), dtype=torch.float32, device=csr.device)
+        self.x_in.zero_()
+        kw = dict(threshold=threshold, hub_threshold=hub_threshold)
+        csr.plan(0, n, threshold, hub_threshold)  # synchronous: never inside the capture
+        side = torch.cuda.Stream(device=csr.device)
+        side.wait_stream(torch.cuda.current_stream(csr.device))
+        with torch.cuda.stream(side):
+            propagate(csr, self.x_in, self.K, out=self.out, **kw)
+        torch.cuda.current_stream(csr.device).wait_stream(side)
+        torch.cuda.synchronize(csr.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            propagate(csr, self.x_in, self.K, out=self.out, **kw)
+
+    def run(self, X: torch.Tensor) -> torch.Tensor:
+        X = _check_features(X, self.csr)
+        if tuple(X.shape) != tuple(self.x_in.shape):
+            raise RuntimeError(f"GraphedPropagation: captured for {tuple(self.x_in.shape)}, "
+                               f"got {tuple(X.shape)}")
+        self.x_in.copy_(X)
+        self.graph.replay()
+        return self.out
+
+
 def linear(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, out=None):
     """Y = X . W^T + b on fp32 MFMA (reference models.py:17-18, nn.Linear)."""
     _require_device(X, "input")

@@ -299,3 +299,27 @@ def test_fused_loss_trains_like_torch():
             opt.step(closure)
         losses.append(torch.nn.functional.cross_entropy(m(X), y).item())
     assert abs(losses[0] - losses[1]) <= 1e-3 * max(1.0, abs(losses[1])), losses
+
+
+@pytest.mark.parametrize("name,K,hub", [("norm_n48_F602", 2, None), ("hub1000_F130", 2, 5),
+                                        ("norm_n48_F65", 1, None)])
+def test_graphed_propagation_bit_exact(tiny_cases, name, K, hub):
+    """The K-hop loop captured into a HIP graph (incl. the hub kernel's
+    side-stream fork/join when hub=5) replays the reference's bits, for two
+    different feature sets through one capture."""
+    from sgc_amd.propagate import DeviceCSR, GraphedPropagation
+    c = tiny_cases[name]
+    csr = DeviceCSR.from_torch(coo_cuda(c))
+    X = torch.from_numpy(c["X"]).to(DEV)
+    g = GraphedPropagation(csr, X.shape, K, threshold=3 if hub else None, hub_threshold=hub)
+    out = g.run(X)
+    torch.cuda.synchronize()
+    assert bits_equal(out.cpu().numpy(), c[f"Y{K}"])
+    X2 = torch.flip(X, dims=[0]).contiguous()
+    from sgc_amd.propagate import propagate
+    want2 = propagate(csr, X2, K).cpu().numpy()
+    out2 = g.run(X2)
+    torch.cuda.synchronize()
+    assert bits_equal(out2.cpu().numpy(), want2)
+    with pytest.raises(RuntimeError):
+        g.run(X[:, :1].contiguous())
