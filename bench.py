@@ -130,7 +130,7 @@ def build_step(args, S, X0, dev, rank, world, distributed, K, output, timing):
 
     if not distributed:
         csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
-        csr.plan(0, n, args.threshold, args.hub_threshold)
+        csr.plan(0, n, args.threshold, args.hub_threshold, F)
         out_buf = torch.empty((n, F), device=dev)
         ev = {}
 

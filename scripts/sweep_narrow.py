@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--max-vec", default="4")
     ap.add_argument("--hub-chunk", default="0")
     ap.add_argument("--hubs", default="auto", help="hub thresholds per case ('auto' = default)")
+    ap.add_argument("--heavies", default="default", help="heavy-row thresholds per case")
+    ap.add_argument("--shape", default="reddit")
     ap.add_argument("--unaligned", action="store_true",
                     help="also read each width straight from the [N, 602] input (ld 602)")
     ap.add_argument("--rounds", type=int, default=5)
@@ -38,14 +40,15 @@ def main():
     libs = [_lib.LIB_PATH] + [p for p in args.libs.split(",") if p]
     loaded = [(os.path.basename(p), _lib.load_path(p)) for p in libs]
     dev = torch.device("cuda", 0)
-    S = graphs.synthetic_graph("reddit", seed=0)
-    F = 602
-    X = torch.from_numpy(graphs.synthetic_features("reddit", S.n, F, seed=1)).to(dev)
+    S = graphs.synthetic_graph(args.shape, seed=0)
+    F = graphs.SHAPES[args.shape]["features"]
+    X = torch.from_numpy(graphs.synthetic_features(args.shape, S.n, F, seed=1)).to(dev)
     csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
     rp = np.asarray(S.row_ptr, dtype=np.int64)
     stream = _lib.stream_handle(dev)
     cases = []
-    for w in (int(x) for x in args.widths.split(",")):
+    widths = [F if x == "F" else int(x) for x in args.widths.split(",")]
+    for w in widths:
         ld = (w + 31) // 32 * 32
         Xw = torch.zeros((S.n, ld), device=dev)
         Xw[:, :w] = X[:, :w]
@@ -54,12 +57,14 @@ def main():
             Y = torch.empty((r1 - r0, ld), device=dev)
             nz = int(rp[r1] - rp[r0])
             gb = (4 * (r1 - r0 + 1) + 8 * nz + 4 * w * nz + 4 * w * (r1 - r0)) / 1e9
-            for hb in args.hubs.split(","):
-                pl = csr.plan(r0, r1, None, None if hb == "auto" else int(hb))
-                cases.append((f"w{w}/P{P}/hub{hb}:{pl.n_hub}", Xw, ld, w, r0, r1, pl, Y, gb))
-                if args.unaligned:
-                    cases.append((f"w{w}/P{P}/hub{hb}:{pl.n_hub}/ld602", X, F, w, r0, r1, pl, Y,
-                                  gb))
+            for hv in args.heavies.split(","):
+                th = None if hv == "default" else int(hv)
+                for hb in args.hubs.split(","):
+                    pl = csr.plan(r0, r1, th, None if hb == "auto" else int(hb), w)
+                    name = f"w{w}/P{P}/heavy{hv}:{pl.n_heavy}/hub{hb}:{pl.n_hub}"
+                    cases.append((name, Xw, ld, w, r0, r1, pl, Y, gb))
+                    if args.unaligned:
+                        cases.append((name + f"/ld{F}", X, F, w, r0, r1, pl, Y, gb))
     mvs = [int(x) for x in args.max_vec.split(",")]
     hcs = [int(x) for x in args.hub_chunk.split(",")]
     variants = [(f"{name}/hc{hc}", lib, (mv, hc)) for name, lib in loaded for mv in mvs

@@ -12,23 +12,35 @@ import torch
 
 from . import _lib
 
-# Rows with more nonzeros than this are split into per-feature-chunk work
+# Schedule (results never depend on it; see sgc_plan_build): rows with more
+# nonzeros than the heavy threshold are split into per-feature-chunk work
 # items and scheduled first; rows above the hub threshold run on the LDS-
-# staged hub kernel (see sgc_plan_build).  Results never depend on either.
-DEFAULT_HEAVY_THRESHOLD = int(os.environ.get("SGC_AMD_HEAVY_THRESHOLD", "512"))
-# Hub threshold: by default a row is a hub when it holds more than 1/1024 of
-# the launch's nonzeros -- i.e. when one wave walking it (~16 nonzeros in
-# flight) would outlast the rest of the launch.  Measured (scripts/
-# rank_work.py --sweep, Reddit shape): the full graph wants ~10 hubs (the
-# 1024-thread hub blocks otherwise queue behind the light rows: 988 hubs cost
-# +20%), a 1/8 row block wants its 132 rows above 2,048 as hubs (-25%).
+# staged hub kernel.  Both default to the launch's size, because what they
+# bound is the tail -- one wave walking a long row with ~16 nonzeros in flight
+# -- against the launch's duration (nnz x F bytes):
+#   heavy = nnz*F / 2^23 to the nearest power of two, clamped to [64, 512];
+#   hub   = max(heavy, nnz / 1024, 256).
+# Measured (scripts/sweep_narrow.py, profiles/r01_heavy_threshold_sweep.log,
+# r01_rank_work_threshold_sweep.log): Reddit full graph 512 / ~10 hubs (988
+# hubs cost +20%); a 1/8 row block 128-256 / its 132 rows above 2,048
+# (-25% vs. no hubs); Pubmed shape 64 / 16 hubs (-25% vs. 512); Cora shape
+# 64 / no hubs (-50%: a 1024-thread hub block costs more than a ~170-nonzero
+# row on one wave).  SGC_AMD_HEAVY_THRESHOLD / SGC_AMD_HUB_THRESHOLD pin them.
+_HEAVY_ENV = os.environ.get("SGC_AMD_HEAVY_THRESHOLD")
+DEFAULT_HEAVY_THRESHOLD = int(_HEAVY_ENV) if _HEAVY_ENV else None
 _HUB_ENV = os.environ.get("SGC_AMD_HUB_THRESHOLD")
 DEFAULT_HUB_THRESHOLD = int(_HUB_ENV) if _HUB_ENV else None
 HUB_SHARE = 1024
 
 
+def auto_heavy_threshold(nnz_range, width):
+    import math
+    work = max(1.0, int(nnz_range) * max(1, int(width)) / float(1 << 23))
+    return int(min(512, max(64, 1 << int(round(math.log2(work))))))
+
+
 def auto_hub_threshold(nnz_range, heavy_threshold):
-    return max(int(heavy_threshold), int(nnz_range) // HUB_SHARE)
+    return max(int(heavy_threshold), int(nnz_range) // HUB_SHARE, 256)
 
 
 class Plan(NamedTuple):
@@ -139,21 +151,31 @@ class DeviceCSR:
         csr.ingest_seconds = time.perf_counter() - t0
         return csr
 
-    def plan(self, row_begin=0, row_end=None, threshold=None, hub_threshold=None) -> Plan:
-        """Heavy-row schedule for rows [row_begin, row_end) (cached)."""
+    def range_nnz(self, row_begin, row_end):
+        """Nonzeros of rows [row_begin, row_end) (cached; reads row_ptr once)."""
+        key = ("nnz", row_begin, row_end)
+        if key not in self._plans:
+            nnz = 0
+            if row_end > row_begin:
+                ends = self.row_ptr[[row_begin, row_end]].tolist()
+                nnz = ends[1] - ends[0]
+            self._plans[key] = nnz
+        return self._plans[key]
+
+    def plan(self, row_begin=0, row_end=None, threshold=None, hub_threshold=None,
+             width=None) -> Plan:
+        """Heavy-row schedule for rows [row_begin, row_end) at `width` features
+        (cached).  Thresholds left None take the size-based defaults above."""
         row_end = self.n_rows if row_end is None else row_end
-        threshold = DEFAULT_HEAVY_THRESHOLD if threshold is None else int(threshold)
+        if threshold is None:
+            threshold = DEFAULT_HEAVY_THRESHOLD
+        if threshold is None:
+            threshold = auto_heavy_threshold(self.range_nnz(row_begin, row_end),
+                                             width if width is not None else 512)
+        threshold = int(threshold)
         hub = DEFAULT_HUB_THRESHOLD if hub_threshold is None else int(hub_threshold)
         if hub is None:
-            auto = self._plans.get(("auto_hub", row_begin, row_end, threshold))
-            if auto is None:
-                nnz = 0
-                if row_end > row_begin:
-                    ends = self.row_ptr[[row_begin, row_end]].tolist()
-                    nnz = ends[1] - ends[0]
-                auto = auto_hub_threshold(nnz, threshold)
-                self._plans[("auto_hub", row_begin, row_end, threshold)] = auto
-            hub = auto
+            hub = auto_hub_threshold(self.range_nnz(row_begin, row_end), threshold)
         hub = max(hub, threshold)
         key = (row_begin, row_end, threshold, hub)
         if key not in self._plans:
@@ -233,7 +255,7 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
         out = torch.empty((row_end - row_begin, F), dtype=torch.float32, device=X.device)
     if F == 0 or row_end == row_begin:
         return out
-    pl = csr.plan(row_begin, row_end, threshold, hub_threshold) if use_plan else NO_PLAN
+    pl = csr.plan(row_begin, row_end, threshold, hub_threshold, F) if use_plan else NO_PLAN
     lib = _lib.load()
     with torch.cuda.device(X.device):
         _lib.check(lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
@@ -273,7 +295,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
         if K <= 0:
             out.copy_(X)
         return out
-    pl = csr.plan(0, n, threshold, hub_threshold) if use_plan else NO_PLAN
+    pl = csr.plan(0, n, threshold, hub_threshold, F) if use_plan else NO_PLAN
     lib = _lib.load()
     stream = _lib.stream_handle(X.device)
     ldw = aligned_ld(F)
@@ -317,9 +339,9 @@ class GraphedPropagation:
     It makes the whole loop -- pad copy, K SpMM launches, the hub kernels'
     fork/join on the side stream -- one replayable unit, e.g. inside a larger
     captured serving step.  It is not a speed-up on its own: even at Pubmed
-    shape a hop is GPU-bound (~70 us of kernel time), and a replay measured
-    191 us against 163 us eager, the static-input copy included
-    (profiles/r01_bench_small.log).  run(X) copies X into the graph's static
+    shape a hop is GPU-bound, and a replay measured 118 us against 122 us
+    eager at K=2, the static-input copy included
+    (profiles/r01_bench_small_v2.log).  run(X) copies X into the graph's static
     input and replays; the result is in self.out (bit-identical to
     propagate()).
     Capture builds the plan first (it synchronises) and warms the code
@@ -334,7 +356,7 @@ class GraphedPropagation:
         self.out = torch.empty((n, F), dtype=torch.float32, device=csr.device)
         self.x_in.zero_()
         kw = dict(threshold=threshold, hub_threshold=hub_threshold)
-        csr.plan(0, n, threshold, hub_threshold)  # synchronous: never inside the capture
+        csr.plan(0, n, threshold, hub_threshold, F)  # synchronous: never inside the capture
         side = torch.cuda.Stream(device=csr.device)
         side.wait_stream(torch.cuda.current_stream(csr.device))
         with torch.cuda.stream(side):
