@@ -275,13 +275,25 @@ def _needs_pad(X):
     return X.stride(0) % 32 != 0 or X.data_ptr() % 128 != 0
 
 
+def pad_pays(csr, F):
+    """Re-lay X_0 into 128-B rows before hop 1?  An unaligned row segment
+    touches about one extra 128-B line per gathered row (32/F of the hop's
+    gather bytes, 128 B per nonzero); the copy moves 8 B per element of X
+    (read + write).  With gathers ~1.2x the streaming rate the copy pays when
+    16 * nnz/N > 1.2 F: Reddit (degree 100, F 602) and RMAT shape yes,
+    Pubmed / Cora shape (degree ~5) no."""
+    n = max(1, csr.n_rows)
+    return 16.0 * csr.range_nnz(0, csr.n_rows) / n > 1.2 * F
+
+
 def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, threshold=None,
               hop_hook=None, native_loop=False, hub_threshold=None):
     """X_K = S^K X on the device (K >= 1); asynchronous on the current stream.
 
     Mirrors sgc_propagate_f32: X is first re-laid into 128-B aligned rows when
-    its rows are not (one streaming copy; each gathered X segment then spans
-    the fewest 128-B lines), hops ping-pong between two aligned buffers, the
+    its rows are not and the copy pays (pad_pays: one streaming copy; each
+    gathered X segment then spans the fewest 128-B lines -- sgc_propagate_f32
+    always copies), hops ping-pong between two aligned buffers, the
     last hop writes the contiguous [N, F] result.  hop_hook(phase, h) is called
     around each hop's launch ("start"/"end", for event timing).
     native_loop=True runs the same loop inside the C ABI call instead."""
@@ -312,7 +324,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
         bufs = [torch.empty((n, ldw), dtype=torch.float32, device=X.device)
                 for _ in range(2 if K >= 2 else 1)]
         src, nxt = X, 0
-        if _needs_pad(X):
+        if _needs_pad(X) and pad_pays(csr, F):
             _lib.check(lib.sgc_pad_rows_f32(_lib.ptr(X), X.stride(0), _lib.ptr(bufs[0]), ldw, n, F,
                                             stream), "pad_rows_f32")
             src, nxt = bufs[0][:, :F], 1 % len(bufs)
