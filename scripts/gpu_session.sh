@@ -30,6 +30,8 @@ for s in $STEPS; do
     dist)   run dist timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
                 --dist-backend gloo ${DIST_ARGS} ;;
+    rdist)  run rdist timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+                --master-addr 127.0.0.1 --master-port 29536 drivers/reddit_dist.py --check --test ;;
     prof)   cd /tmp && export TMPDIR=/tmp && \
             run prof timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
                 --output-format csv -- python3 "$ROOTDIR/bench.py" --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS}
