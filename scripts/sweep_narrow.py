@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--parts", default="1,8")
     ap.add_argument("--max-vec", default="4")
     ap.add_argument("--hub-chunk", default="0")
+    ap.add_argument("--hub-priority", default="1")
     ap.add_argument("--hubs", default="auto", help="hub thresholds per case ('auto' = default)")
     ap.add_argument("--heavies", default="default", help="heavy-row thresholds per case")
     ap.add_argument("--shape", default="reddit")
@@ -67,14 +68,16 @@ def main():
                         cases.append((name + f"/ld{F}", X, F, w, r0, r1, pl, Y, gb))
     mvs = [int(x) for x in args.max_vec.split(",")]
     hcs = [int(x) for x in args.hub_chunk.split(",")]
-    variants = [(f"{name}/hc{hc}", lib, (mv, hc)) for name, lib in loaded for mv in mvs
-                for hc in hcs]
+    hps = [int(x) for x in args.hub_priority.split(",")]
+    variants = [(f"{name}/hc{hc}/hp{hp}", lib, (mv, hc, hp)) for name, lib in loaded for mv in mvs
+                for hc in hcs for hp in hps]
 
     def run(lib, cfg, c):
-        mv, hc = cfg
+        mv, hc, hp = cfg
         _, Xw, ld, w, r0, r1, pl, Y, _ = c
         lib.sgc_set_tuning(b"max_vec", mv)
         lib.sgc_set_tuning(b"hub_chunk", hc)
+        lib.sgc_set_tuning(b"hub_priority", hp)
         rc = lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val),
                                   r0, r1, _lib.ptr(Xw), ld, _lib.ptr(Y), Y.stride(0), w,
                                   _lib.ptr(pl.rows),

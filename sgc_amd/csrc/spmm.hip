@@ -314,16 +314,31 @@ struct SideStream {
     hipEvent_t fork = nullptr, join = nullptr;
 };
 
+// Hub-kernel stream priority: 1 = the device's highest (meant to let a
+// waiting hub workgroup -- a whole CU's worth of LDS and 16 waves -- be placed
+// before further light-row workgroups), 0 = normal.  Measured neutral (+-1%,
+// profiles/r01_hub_priority_sweep.log), so the default is 0.  Set through
+// sgc_set_tuning("hub_priority").
+static int g_hub_priority = 0;
+
 hipError_t side_stream(SideStream **out) {
     static std::mutex mu;
-    static std::map<int, SideStream> per_dev;
+    static std::map<std::pair<int, int>, SideStream> per_dev;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> lock(mu);
-    SideStream &ss = per_dev[dev];
+    SideStream &ss = per_dev[{dev, g_hub_priority}];
     if (!ss.s) {
-        if ((e = hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking)) != hipSuccess) return e;
+        if (g_hub_priority) {
+            int least = 0, greatest = 0;
+            if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return e;
+            if ((e = hipStreamCreateWithPriority(&ss.s, hipStreamNonBlocking, greatest)) !=
+                hipSuccess)
+                return e;
+        } else if ((e = hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking)) != hipSuccess) {
+            return e;
+        }
         if ((e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming)) != hipSuccess) return e;
         if ((e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming)) != hipSuccess) return e;
     }
@@ -400,6 +415,11 @@ int set_tuning(const char *key, int64_t value) {
         g_hub_chunk = (int)value;
         return SGC_OK;
     }
+    if (std::string(key) == "hub_priority") {
+        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "hub_priority must be 0 or 1");
+        g_hub_priority = (int)value;
+        return SGC_OK;
+    }
     if (std::string(key) == "max_vec") {
         SGC_REQUIRE(value == 1 || value == 2 || value == 4, SGC_EINVAL, "max_vec must be 1, 2 or 4");
         g_max_vec = (int)value;
@@ -413,6 +433,7 @@ int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "slice_floats") return g_slice_floats;
     if (key && std::string(key) == "max_vec") return g_max_vec;
     if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
+    if (key && std::string(key) == "hub_priority") return g_hub_priority;
     return -1;
 }
 
