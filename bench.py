@@ -329,7 +329,8 @@ def main():
             "precompute_seconds": ms_per_step / 1e3,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "spmm_csr_kernel", "kernel_mean_ms": kern_mean_ms,
+                         "kernel": "spmm_csr_kernel + spmm_hub_kernel (side stream, joined)",
+                         "kernel_mean_ms": kern_mean_ms,
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "launch_unit": unit_desc, "traffic_source": traffic_src,
                          "compulsory_bytes_per_hop": 4 * (n + 1) + 8 * nnz + 8 * F * n},
