@@ -237,7 +237,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threshold", type=int, default=None, help="heavy-row threshold")
     ap.add_argument("--hub-threshold", type=int, default=None, help="hub-row threshold")
-    ap.add_argument("--group-floats", type=int, default=320,
+    ap.add_argument("--group-floats", type=int, default=224,
                     help="N>1 rows: feature-group width of the compute/all-gather pipeline")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged rehearsal of the N>1 path (ranks may share a GPU)")

@@ -187,21 +187,25 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 //    and writes them with four ds_write_b128;
 //  * loaders keep kHubDepth rounds in registers: round t+kHubDepth is issued
 //    while round t+1 is written, so a load has kHubDepth-1 rounds of FMA time
-//    to land (a round is ~0.5 us of chain; an HBM/IC gather ~1-2 us).
+//    to land (a round is ~0.5 us of chain; an HBM/IC gather ~1-2 us), and the
+//    column ids of a round arrive one round before its X loads.
 // HC = 32 (one 128-B line per nonzero; lanes 32-63 load the second 16
 // nonzeros of the loader's run) halves the bytes each block ingests per
 // nonzero and spreads a hub over twice the CUs; it needs 128-B aligned X rows
 // to stay one line per segment.
 constexpr int kHubLoaders = 15;
 constexpr int kHubInstr = 16;  // consecutive nonzeros per loader lane per round
-constexpr int kHubDepth = 3;   // rounds held in loader registers
+constexpr int kHubDepth = 3;   // rounds held in loader registers (17 loads each: vmcnt <= 63)
+constexpr int kHubUnroll = 6;  // lcm(kHubDepth, 2): X ring slot and colv parity compile-time
 
 template <int HC>
 struct HubShape {
     static constexpr int kSegs = kWave / HC;                     // nonzero runs per loader wave
     static constexpr int kPerLoader = kHubInstr * kSegs;         // nonzeros per loader per round
     static constexpr int kRound = kHubLoaders * kPerLoader;      // nonzeros per round (240 / 480)
-    static constexpr int kStride = (kRound + 63) / 64 * 64 + 4;  // dwords per gxT row (4 mod 64)
+    // dwords per gxT row: 4 mod 64 (conflict-free b128), and >= kRound + 12 for
+    // the FMA loop's read-ahead (3 batches of 4 past the last full batch)
+    static constexpr int kStride = (kRound + 12 + 63) / 64 * 64 + 4;
 };
 
 template <int HC>
@@ -212,7 +216,7 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
     using Sh = HubShape<HC>;
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) float gxT[2][HC * Sh::kStride];  // 2 x 66.5 KB
-    __shared__ __attribute__((aligned(16))) float gv[2][Sh::kRound];
+    __shared__ __attribute__((aligned(16))) float gv[2][Sh::kRound + 12];  // + read-ahead
     const int lane = threadIdx.x & (kWave - 1);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
     const int h = blockIdx.x / n_chunks;
@@ -226,18 +230,31 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
     const char *Xb = reinterpret_cast<const char *>(X);
     const int64_t row_bytes = ldx * 4;
     const int n_round = (k1 - k0 + Sh::kRound - 1) / Sh::kRound;
+    const int my_k = lane & (Sh::kPerLoader - 1);  // this lane's nonzero of the loader's run
     float regs[kHubDepth][kHubInstr];
     float vreg[kHubDepth];
-    // loader waves only; `s` is always a compile-time constant after unrolling
-    auto load = [&](int r, int s) {
+    int colv[2];  // column ids of the loader's run, one per lane, for two future rounds
+    // Loader waves only; `s` and `p` are compile-time constants after unrolling.
+    // Column ids come in with ONE coalesced load per round (lane j holds
+    // nonzero j's id, broadcast with v_readlane), issued a round before the X
+    // loads that use them (per-nonzero scalar loads, each waited on, cost
+    // ~0.4 us per round: 493 -> 406 us on the 47,857-nonzero row).
+    auto load_col = [&](int r, int p) {
         const int kr = k0 + r * Sh::kRound + (w - 1) * Sh::kPerLoader;
-        const int kb = kr + seg * kHubInstr;
+        colv[p] = col[min(kr + my_k, k1 - 1)];
+    };
+    auto load_x = [&](int r, int s, int p) {
+        const int kr = k0 + r * Sh::kRound + (w - 1) * Sh::kPerLoader;
 #pragma unroll
         for (int j = 0; j < kHubInstr; ++j) {
-            const int cj = col[min(kb + j, k1 - 1)];
+            int cj = __builtin_amdgcn_readlane(colv[p], j);
+            if (HC == 32) {
+                const int c1 = __builtin_amdgcn_readlane(colv[p], kHubInstr + j);
+                cj = seg ? c1 : cj;
+            }
             regs[s][j] = *reinterpret_cast<const float *>(Xb + (int64_t)cj * row_bytes + boff);
         }
-        vreg[s] = val[min(kr + (lane & (Sh::kPerLoader - 1)), k1 - 1)];
+        vreg[s] = val[min(kr + my_k, k1 - 1)];
     };
     auto store = [&](int buf, int s) {
         f4 *dst = reinterpret_cast<f4 *>(
@@ -247,36 +264,75 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
             dst[q] = f4{regs[s][4 * q], regs[s][4 * q + 1], regs[s][4 * q + 2], regs[s][4 * q + 3]};
         if (lane < Sh::kPerLoader) gv[buf][(w - 1) * Sh::kPerLoader + lane] = vreg[s];
     };
+    // Loads are never predicated (rounds past the row re-read its last
+    // nonzero): a conditional load makes its registers a phi, and copying a
+    // phi waits for every load in flight.
     if (w > 0) {
 #pragma unroll
-        for (int s = 0; s < kHubDepth; ++s)
-            if (s < n_round) load(s, s);
+        for (int s = 0; s < kHubDepth; ++s) {
+            load_col(s, s & 1);
+            load_x(s, s, s & 1);
+        }
+        load_col(kHubDepth, kHubDepth & 1);
         if (n_round > 0) store(0, 0);
     }
     __syncthreads();
     float acc = 0.0f;
-    for (int r0 = 0; r0 < n_round; r0 += kHubDepth) {
+    for (int r0 = 0; r0 < n_round; r0 += kHubUnroll) {
 #pragma unroll
-        for (int s = 0; s < kHubDepth; ++s) {
-            const int r = r0 + s;  // round t lives in regs[t % kHubDepth]
+        for (int s = 0; s < kHubUnroll; ++s) {
+            // round t's X lives in regs[t % kHubDepth], its column ids in colv[t & 1]
+            const int r = r0 + s;
             if (r >= n_round) break;  // block-uniform
             const int buf = r & 1;
+#ifndef SGC_HUB_EXPERIMENT
+#define SGC_HUB_EXPERIMENT 0  // timing probes only: 1 = no FMA chain, 2 = no X loads
+#endif
             if (w > 0) {
                 if (r + 1 < n_round) store(buf ^ 1, (s + 1) % kHubDepth);
-                if (r + kHubDepth < n_round) load(r + kHubDepth, s);
-            } else {
+                // ids of round r+D+1 first, so waiting for them (next round)
+                // does not also wait for this round's X loads
+                if (SGC_HUB_EXPERIMENT != 2) {
+                    load_col(r + kHubDepth + 1, (s + kHubDepth + 1) & 1);
+                    load_x(r + kHubDepth, s % kHubDepth, (s + kHubDepth) & 1);
+                }
+            } else if (SGC_HUB_EXPERIMENT != 1) {
                 const int n = min(Sh::kRound, k1 - (k0 + r * Sh::kRound));
                 const f4 *xs = reinterpret_cast<const f4 *>(&gxT[buf][fl * Sh::kStride]);
                 const f4 *vs = reinterpret_cast<const f4 *>(&gv[buf][0]);
                 const int n4 = n >> 2;
-#pragma unroll 4
-                for (int q = 0; q < n4; ++q) {
-                    const f4 x = xs[q], v = vs[q];
-                    acc = __builtin_fmaf(v[0], x[0], acc);
-                    acc = __builtin_fmaf(v[1], x[1], acc);
-                    acc = __builtin_fmaf(v[2], x[2], acc);
-                    acc = __builtin_fmaf(v[3], x[3], acc);
+                // LDS reads run kPre batches of four nonzeros ahead of the FMA
+                // chain (a ds_read's ~64-cycle latency otherwise lands on the
+                // chain every four FMAs); reads past n stay inside the padded
+                // row / value buffers (kStride, gv) and are never used.
+                constexpr int kPre = 3;
+                f4 xq[kPre], vq[kPre];
+#pragma unroll
+                for (int i = 0; i < kPre; ++i) {
+                    xq[i] = xs[i];
+                    vq[i] = vs[i];
                 }
+                int q = 0;
+                for (; q + kPre <= n4; q += kPre) {
+#pragma unroll
+                    for (int i = 0; i < kPre; ++i) {
+                        const f4 x = xq[i], v = vq[i];
+                        xq[i] = xs[q + kPre + i];
+                        vq[i] = vs[q + kPre + i];
+                        acc = __builtin_fmaf(v[0], x[0], acc);
+                        acc = __builtin_fmaf(v[1], x[1], acc);
+                        acc = __builtin_fmaf(v[2], x[2], acc);
+                        acc = __builtin_fmaf(v[3], x[3], acc);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < kPre; ++i)
+                    if (q + i < n4) {
+                        acc = __builtin_fmaf(vq[i][0], xq[i][0], acc);
+                        acc = __builtin_fmaf(vq[i][1], xq[i][1], acc);
+                        acc = __builtin_fmaf(vq[i][2], xq[i][2], acc);
+                        acc = __builtin_fmaf(vq[i][3], xq[i][3], acc);
+                    }
                 const float *xt = &gxT[buf][fl * Sh::kStride];
                 for (int kk = n4 * 4; kk < n; ++kk) acc = __builtin_fmaf(gv[buf][kk], xt[kk], acc);
             }

@@ -125,7 +125,7 @@ class RowPartitionedPropagator:
     columns are computed and never returned)."""
 
     def __init__(self, shard: ShardCSR, group=None, spmm_fn: Optional[Callable] = None,
-                 group_floats: int = 320, host_staging: bool = False,
+                 group_floats: int = 224, host_staging: bool = False,
                  pad_input: Optional[bool] = None):
         self.shard = shard
         # Re-lay X_0 into 128-B rows before hop 1?  The copy (all N rows, ~0.2 ms
