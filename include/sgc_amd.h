@@ -42,12 +42,15 @@ int sgc_abi_version(void);
 const char *sgc_last_error(void);
 
 /* Process-wide schedule knobs (results never depend on them).
- *   "slice_floats": feature-slice width of the SpMM grid (default 0:
- *                   0 = one slice as wide as the registers allow);
+ *   "slice_floats": feature-slice width of the SpMM grid in floats (default
+ *                   128 = one 64V-float chunk per slice; 0 = one slice as wide
+ *                   as the registers allow);
  *   "max_vec":      widest per-lane load, 1, 2 or 4 floats (default 4);
  *   "hub_chunk":    features per hub-kernel workgroup, 32 or 64 (default 0 =
  *                   32 when F <= 192 and X rows are 128-B aligned, else 64);
- *   "hub_priority": 1 = hub kernel on a highest-priority stream (default 0).
+ *   "hub_priority": 1 = hub kernel on a highest-priority stream (default 0);
+ *   "hub_first":    1 = hub kernel on the caller's stream, the light/heavy
+ *                   kernel on the side stream (default 0: the reverse).
  * sgc_get_tuning returns -1 for an unknown key. */
 int sgc_set_tuning(const char *key, int64_t value);
 int64_t sgc_get_tuning(const char *key);

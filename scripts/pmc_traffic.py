@@ -30,6 +30,8 @@ sys.path.insert(0, ROOT)
 
 N_CAL = 1_000_000
 F = 602
+LD = 608     # X / Y row stride as propagate() lays them out: 128-B rows
+LINES = (4 * F + 127) // 128  # 128-B lines one row's F floats touch (19)
 REPEATS = 3
 
 
@@ -45,8 +47,8 @@ def workload():
     ci = np.arange(N_CAL, dtype=np.int32)
     va = np.ones(N_CAL, dtype=np.float32)
     cal = DeviceCSR.from_host_arrays(rp, ci, va, device=dev)
-    Xc = torch.randn((N_CAL, F), device=dev)
-    Yc = torch.empty_like(Xc)
+    Xc = torch.randn((N_CAL, LD), device=dev)[:, :F]
+    Yc = torch.empty((N_CAL, LD), device=dev)[:, :F]
     for _ in range(REPEATS):
         spmm(cal, Xc, out=Yc, use_plan=False)
     torch.cuda.synchronize()
@@ -58,9 +60,10 @@ def workload():
         if v is not None:
             lib.sgc_set_tuning(key.encode(), int(v))
     S = graphs.synthetic_graph("reddit", seed=0)
-    X = torch.from_numpy(graphs.synthetic_features("reddit", S.n, F, seed=1)).to(dev)
+    X = torch.zeros((S.n, LD), device=dev)[:, :F]
+    X.copy_(torch.from_numpy(graphs.synthetic_features("reddit", S.n, F, seed=1)))
     csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
-    Y = torch.empty_like(X)
+    Y = torch.empty((S.n, LD), device=dev)[:, :F]
     for _ in range(REPEATS):
         spmm(csr, X, out=Y)
     torch.cuda.synchronize()
@@ -123,8 +126,10 @@ def summarize(out_dir):
     def mean(d, ks):  # ks: dispatch ids, or groups of ids summed per launch
         vals = [sum(d[j][2] for j in k) if isinstance(k, list) else d[k][2] for k in ks]
         return sum(vals) / max(1, len(vals))
-    known_read = 4 * F_ * n_cal + 4 * (n_cal + 1) + 8 * n_cal
-    known_write = 4 * F_ * n_cal
+    # line-granular: every X row touched once (LINES whole 128-B lines of its
+    # 128-B aligned LD-float row), every Y row written once, plus the CSR
+    known_read = 128 * LINES * n_cal + 4 * (n_cal + 1) + 8 * n_cal
+    known_write = 128 * LINES * n_cal
     cal_fetch_b = mean(fetch, cal_f) * 1024
     cal_write_b = mean(write, cal_w) * 1024
     read_factor = known_read / cal_fetch_b
@@ -141,12 +146,13 @@ def summarize(out_dir):
     n, nnz = meta.get("n", 232965), meta.get("nnz", 23446803)
     alg = 4 * (n + 1) + 8 * nnz + 4 * F_ * nnz + 4 * F_ * n
     rec = {
-        "workload": "reddit-shape spmm hop (232,965 rows, 23,446,803 nnz, F=602)",
+        "workload": "reddit-shape spmm hop (232,965 rows, 23,446,803 nnz, F=602, X/Y ld 608 "
+                    "as propagate() lays them out)",
         "hbm_bytes_per_launch": red_fetch_b + red_write_b,
         "hbm_read_bytes_per_launch": red_fetch_b,
         "hbm_write_bytes_per_launch": red_write_b,
         "raw_FETCH_SIZE_kB": mean(fetch, red_f), "raw_WRITE_SIZE_kB": mean(write, red_w),
-        "calibration": {"kernel": "same spmm kernel over identity S", "rows": n_cal,
+        "calibration": {"kernel": "same spmm kernel over identity S, ld 608", "rows": n_cal,
                         "known_read_bytes": known_read, "known_write_bytes": known_write,
                         "FETCH_SIZE_bytes": cal_fetch_b, "WRITE_SIZE_bytes": cal_write_b,
                         "read_factor": read_factor, "write_factor": write_factor},

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--thresholds", default="2048")
     ap.add_argument("--hubs", default="4096", help="hub thresholds (sgc_plan_build)")
     ap.add_argument("--slices", default="128", help="slice_floats values (sgc_set_tuning)")
+    ap.add_argument("--vecs", default="4", help="max_vec values (sgc_set_tuning)")
+    ap.add_argument("--knob", default="", help="one more sgc_set_tuning key: name=v1,v2")
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--shape", default="reddit")
@@ -54,12 +56,19 @@ def main():
     stream = _lib.stream_handle(dev)
     ref = None
     slices = [int(x) for x in args.slices.split(",")]
-    variants = [(f"{name}/s{sf}/ld{ld}/hub{hb}", lib, t, (sf, ld, hb)) for name, lib in loaded
-                for t in thresholds for sf in slices for ld in lds for hb in hubs]
+    vecs = [int(x) for x in args.vecs.split(",")]
+    kname, kvals = (args.knob.split("=") + [""])[:2] if args.knob else ("", "")
+    kvals = [int(x) for x in kvals.split(",")] if kname else [None]
+    variants = [(f"{name}/v{mv}/s{sf}/ld{ld}/hub{hb}" + (f"/{kname}{kv}" if kname else ""), lib, t,
+                 (sf, ld, hb, mv, kv)) for name, lib in loaded for t in thresholds for sf in slices
+                for ld in lds for hb in hubs for mv in vecs for kv in kvals]
 
     def run(lib, t, cfg):
-        sf, ld, hb = cfg
+        sf, ld, hb, mv, kv = cfg
         lib.sgc_set_tuning(b"slice_floats", sf)
+        lib.sgc_set_tuning(b"max_vec", mv)
+        if kname and lib.sgc_set_tuning(kname.encode(), kv):
+            raise RuntimeError(lib.sgc_last_error())
         pl = plans[(t, hb)]
         rc = lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val),
                                   0, S.n, _lib.ptr(Xs[ld]), ld, _lib.ptr(Y), F, F, _lib.ptr(pl.rows),

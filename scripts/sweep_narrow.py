@@ -29,7 +29,8 @@ def main():
     ap.add_argument("--parts", default="1,8")
     ap.add_argument("--max-vec", default="4")
     ap.add_argument("--hub-chunk", default="0")
-    ap.add_argument("--hub-priority", default="1")
+    ap.add_argument("--hub-priority", default="0")
+    ap.add_argument("--slices", default="128", help="slice_floats values")
     ap.add_argument("--hubs", default="auto", help="hub thresholds per case ('auto' = default)")
     ap.add_argument("--heavies", default="default", help="heavy-row thresholds per case")
     ap.add_argument("--shape", default="reddit")
@@ -69,11 +70,13 @@ def main():
     mvs = [int(x) for x in args.max_vec.split(",")]
     hcs = [int(x) for x in args.hub_chunk.split(",")]
     hps = [int(x) for x in args.hub_priority.split(",")]
-    variants = [(f"{name}/hc{hc}/hp{hp}", lib, (mv, hc, hp)) for name, lib in loaded for mv in mvs
-                for hc in hcs for hp in hps]
+    sfs = [int(x) for x in args.slices.split(",")]
+    variants = [(f"{name}/hc{hc}/hp{hp}/s{sf}", lib, (mv, hc, hp, sf)) for name, lib in loaded
+                for mv in mvs for hc in hcs for hp in hps for sf in sfs]
 
     def run(lib, cfg, c):
-        mv, hc, hp = cfg
+        mv, hc, hp, sf = cfg
+        lib.sgc_set_tuning(b"slice_floats", sf)
         _, Xw, ld, w, r0, r1, pl, Y, _ = c
         lib.sgc_set_tuning(b"max_vec", mv)
         lib.sgc_set_tuning(b"hub_chunk", hc)

@@ -128,6 +128,124 @@ __device__ __forceinline__ void row_chunks(const int *__restrict__ col,
         }
 }
 
+// CSR (col, val) loads: streamed once per slice; SGC_NT_META marks them
+// non-temporal so they need not displace X lines in L2 / the Infinity Cache.
+template <typename T>
+__device__ __forceinline__ T ld_meta(const T *p) {
+#if SGC_NT_META
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
+// Software-pipelined form of row_chunks: the X segments of step s+1 (U
+// nonzeros) are issued before the FMAs of step s, so a wave always has one
+// to two steps of gathers in flight instead of draining to zero between
+// steps; the (col, val) block of the next 64 nonzeros is loaded one block
+// ahead.  Loads are never predicated (a predicated load's phi copy would
+// wait for every load in flight): indices past the row clamp to its last
+// nonzero (same lines, no extra traffic) and only the FMAs are skipped, with
+// wave-uniform branches.  Same FMA order as row_chunks.
+template <int V, int C, int U>
+__device__ __forceinline__ void row_chunks_pipe(const int *__restrict__ col,
+                                                const float *__restrict__ val, int k0, int k1,
+                                                const float *__restrict__ X, int64_t ldx,
+                                                float *__restrict__ yrow, int F, int chunk0,
+                                                int lane) {
+    using VT = typename Vec<V>::T;
+    constexpr int kSteps = kWave / U;  // steps per 64-nonzero block
+    static_assert(kWave % U == 0 && kSteps % 2 == 0, "U must divide 64 into an even count");
+    uint32_t boff[C];
+    bool ok[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const int f = (chunk0 + c) * (kWave * V) + lane * V;
+        ok[c] = f < F;
+        boff[c] = ok[c] ? uint32_t(f) * 4u : 0u;
+    }
+    VT acc[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+        for (int v = 0; v < V; ++v) set_elem<V>(acc[c], v, 0.0f);
+
+    if (k1 > k0) {
+        const char *Xb = reinterpret_cast<const char *>(X);
+        const int64_t row_bytes = ldx * 4;
+        const int last = k1 - 1;
+        // (col, val) of blocks b (A) and b+1 (B); clamped, never predicated
+        int colA = ld_meta(col + min(k0 + lane, last));
+        float valA = ld_meta(val + min(k0 + lane, last));
+        int colB = ld_meta(col + min(k0 + kWave + lane, last));
+        float valB = ld_meta(val + min(k0 + kWave + lane, last));
+        VT xv[2][U][C];
+        float vv[2][U];
+        // step (block base, step i) -> buffer i & 1; lanes of the block in colA/colB
+        auto issue = [&](int base, int i, int colr, float valr, int buf) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = min(base + i * U + u, last);
+                const int l = (k - base) & (kWave - 1);  // clamped past the row: any lane
+                                                         // of colr holds a valid column
+                const int cj = __builtin_amdgcn_readlane(colr, l);
+                vv[buf][u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(valr), l));
+                const char *xr = Xb + (int64_t)cj * row_bytes;
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    xv[buf][u][c] = *reinterpret_cast<const VT *>(xr + boff[c]);
+            }
+        };
+        issue(k0, 0, colA, valA, 0);
+        for (int base = k0;; base += kWave) {
+#pragma unroll
+            for (int i = 0; i < kSteps; ++i) {
+                const int cur = base + i * U;
+                if (cur > last) break;  // uniform; the step issued for it is dropped
+                if (i + 1 < kSteps)
+                    issue(base, i + 1, colA, valA, (i + 1) & 1);
+                else  // first step of the next block, from its prefetched (col, val)
+                    issue(base + kWave, 0, colB, valB, 0);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (cur + u <= last) {
+#pragma unroll
+                        for (int c = 0; c < C; ++c)
+#pragma unroll
+                            for (int v = 0; v < V; ++v)
+                                set_elem<V>(acc[c], v,
+                                            __builtin_fmaf(vv[i & 1][u],
+                                                           lane_elem<V>(xv[i & 1][u][c], v),
+                                                           lane_elem<V>(acc[c], v)));
+                    }
+                }
+            }
+            if (base + kWave > last) break;
+            colA = colB;
+            valA = valB;
+            colB = ld_meta(col + min(base + 2 * kWave + lane, last));
+            valB = ld_meta(val + min(base + 2 * kWave + lane, last));
+        }
+    }
+    char *Yb = reinterpret_cast<char *>(yrow);
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+        if (ok[c]) {
+#if SGC_NT_STORE
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                __builtin_nontemporal_store(lane_elem<V>(acc[c], v),
+                                            reinterpret_cast<float *>(Yb + boff[c]) + v);
+#else
+            *reinterpret_cast<VT *>(Yb + boff[c]) = acc[c];
+#endif
+        }
+}
+
+#ifndef SGC_PIPE
+#define SGC_PIPE 1
+#endif
+
 // Grid: x = work items of one feature slice, y = slice.  Workgroups are
 // dispatched x-fastest, so the chip sweeps the slices one after another and
 // only X[:, slice] (N x 64CV floats -- 119 MB at Reddit shape for 128
@@ -158,8 +276,13 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
         if (sub * kWave * VH >= F) return;
         const int row = heavy_rows[h];
         const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
+#if SGC_PIPE
+        row_chunks_pipe<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
+                                        Y + (int64_t)(row - row_begin) * ldy, F, sub, lane);
+#else
         row_chunks<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
                                    Y + (int64_t)(row - row_begin) * ldy, F, sub, lane);
+#endif
         return;
     }
     const int r = wave - n_heavy_items;
@@ -167,7 +290,11 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int row = row_begin + r;
     const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
     if (k1 - k0 > heavy_threshold) return;  // done as a heavy item or by the hub kernel
+#if SGC_PIPE
+    row_chunks_pipe<V, C, U>(col, val, k0, k1, X, ldx, Y + (int64_t)r * ldy, F, slice * C, lane);
+#else
     row_chunks<V, C, U>(col, val, k0, k1, X, ldx, Y + (int64_t)r * ldy, F, slice * C, lane);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -402,13 +529,15 @@ hipError_t side_stream(SideStream **out) {
     return hipSuccess;
 }
 
-// Nonzeros in flight per wave: light items keep U*C*V <= ~40 registers of
-// gathered X; heavy sub-chunk items (one float per lane) go deeper (UH).
+// Nonzeros per step: light items keep U*C*V <= ~40 registers of gathered X
+// per step; heavy sub-chunk items go deeper (UH).  The pipelined loop holds
+// two steps, so it halves U (measured best at 8 / 16: 48 VGPRs, 8 waves per
+// SIMD, -3% per hop vs. the unpipelined U = 16 / 32; profiles/r01_sweep_pipe.log).
 #ifndef SGC_LIGHT_U_SCALE
-#define SGC_LIGHT_U_SCALE 2
+#define SGC_LIGHT_U_SCALE (SGC_PIPE ? 1 : 2)
 #endif
 #ifndef SGC_HEAVY_U
-#define SGC_HEAVY_U 32
+#define SGC_HEAVY_U (SGC_PIPE ? 16 : 32)
 #endif
 template <int V, int C>
 hipError_t launch_vc(const LaunchArgs &a) {
@@ -452,11 +581,21 @@ constexpr int max_chunks(int V) { return 16 / V; }  // <= 16 accumulators per la
 
 }  // namespace
 
-// Slice width in 64V-float chunks; 0 = widest the registers allow (one
-// slice for F <= 64*16).  Set through sgc_set_tuning("slice_floats", n).
-static int g_slice_floats = 0;
+// Feature-slice width in floats (rounded down to whole 64V-float chunks,
+// at least one).  Default 128: one chunk per slice, so the chip's pass over
+// S touches only X[:, slice] -- 119 MB at the Reddit shape, resident in the
+// 256 MB MALL -- at the price of re-reading the CSR once per slice (8 B/nnz).
+// Measured 4.74 ms/hop at the Reddit shape vs 5.48 ms for 256 and 6.24 ms
+// for 0 = one slice as wide as the registers allow (2.9 GB live X)
+// (profiles/r01_sweep_slices.log).  Set through sgc_set_tuning("slice_floats", n).
+static int g_slice_floats = 128;
 // Hub-kernel feature chunk: 0 = auto (32 on 128-B aligned X rows, else 64).
 static int g_hub_chunk = 0;
+// Which kernel goes first: 0 = hub kernel on the side stream (it starts after
+// the fork-event wait, once the light rows' workgroups hold every CU), 1 = hub
+// kernel on the caller's stream, light/heavy kernel on the side stream (the
+// hub workgroups are placed first).  Set through sgc_set_tuning("hub_first").
+static int g_hub_first = 0;
 
 int set_tuning(const char *key, int64_t value) {
     SGC_REQUIRE(key, SGC_EINVAL, "set_tuning: null key");
@@ -476,6 +615,11 @@ int set_tuning(const char *key, int64_t value) {
         g_hub_priority = (int)value;
         return SGC_OK;
     }
+    if (std::string(key) == "hub_first") {
+        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "hub_first must be 0 or 1");
+        g_hub_first = (int)value;
+        return SGC_OK;
+    }
     if (std::string(key) == "max_vec") {
         SGC_REQUIRE(value == 1 || value == 2 || value == 4, SGC_EINVAL, "max_vec must be 1, 2 or 4");
         g_max_vec = (int)value;
@@ -490,6 +634,7 @@ int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "max_vec") return g_max_vec;
     if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
     if (key && std::string(key) == "hub_priority") return g_hub_priority;
+    if (key && std::string(key) == "hub_first") return g_hub_first;
     return -1;
 }
 
@@ -524,13 +669,14 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         SGC_HIP_CHECK(side_stream(&side));
         SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
         SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
+        hipStream_t hs = g_hub_first ? stream : side->s;
         if (hc == 32)
             hipLaunchKernelGGL(spmm_hub_kernel<32>, dim3((unsigned)(n_hub * n_chunks)), dim3(1024),
-                               0, side->s, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
+                               0, hs, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
                                (int)F, heavy_rows, n_chunks);
         else
             hipLaunchKernelGGL(spmm_hub_kernel<64>, dim3((unsigned)(n_hub * n_chunks)), dim3(1024),
-                               0, side->s, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
+                               0, hs, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
                                (int)F, heavy_rows, n_chunks);
         SGC_HIP_CHECK(hipGetLastError());
         heavy_rows += n_hub;
@@ -548,7 +694,8 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     SGC_REQUIRE(slices < 65536, SGC_ERANGE, "spmm: too many feature slices");
 
     LaunchArgs a{row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)n_rows, (int)F,
-                 heavy_rows, (int)n_heavy, heavy_threshold, slices, stream};
+                 heavy_rows, (int)n_heavy, heavy_threshold, slices,
+                 side && g_hub_first ? side->s : stream};
     hipError_t e;
     if (V == 4)
         e = dispatch_c<4, max_chunks(4)>(C, a);
