@@ -185,13 +185,21 @@ def build_step(args, S, X0, dev, rank, world, distributed, K, output, timing):
             fg = X.shape[1]
             return 4 * (sh.rows + 1) + 8 * nnz_l + 4 * fg * nnz_l + 4 * fg * sh.rows
 
+        auto = args.group_floats == "auto"
         prop = RowPartitionedPropagator(shard, spmm_fn=bracket(_default_spmm, launch_bytes),
-                                        group_floats=args.group_floats, host_staging=staging)
+                                        group_floats=224 if auto else int(args.group_floats),
+                                        host_staging=staging)
+        tuned = ""
+        if auto:  # untimed setup, like the plans: every rank picks the same width
+            tt = prop.autotune(X0, K, output=output)
+            tuned = " (autotuned: " + ", ".join(f"{g}: {t * 1e3:.2f} ms"
+                                                for g, t in tt.items()) + ")"
+        gf = prop.group_floats
         exch = ("all-gather of X_k after each hop but the last" if output == "sharded" else
                 "all-gather of X_k after every hop")
         par = (f"row-partition x{world} (equal-row blocks) + {backend} {exch}, pipelined in "
-               f"{args.group_floats}-float feature groups; output {output}")
-        unit = (f"one hop of one {args.group_floats}-float feature group over rank 0's "
+               f"{gf}-float feature groups{tuned}; output {output}")
+        unit = (f"one hop of one {gf}-float feature group over rank 0's "
                 f"{shard.rows} rows ({nnz_l} nnz)")
     out = None
     if output == "replicated":
@@ -237,8 +245,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threshold", type=int, default=None, help="heavy-row threshold")
     ap.add_argument("--hub-threshold", type=int, default=None, help="hub-row threshold")
-    ap.add_argument("--group-floats", type=int, default=224,
-                    help="N>1 rows: feature-group width of the compute/all-gather pipeline")
+    ap.add_argument("--group-floats", default="auto",
+                    help="N>1 rows: feature-group width of the compute/all-gather pipeline "
+                         "(an integer, or auto = timed on this node among 224/304/160)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged rehearsal of the N>1 path (ranks may share a GPU)")
     ap.add_argument("--distributed-path", action="store_true",

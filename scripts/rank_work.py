@@ -55,7 +55,7 @@ def sweep(csr, X0, n, F, reps, heavies, hubs):
         out = torch.empty((r1 - r0, X.shape[1]), device="cuda")
         for th in heavies:
             for hb in hubs:
-                pl = csr.plan(r0, r1, th, hb)
+                pl = csr.plan(r0, r1, th, hb, X.shape[1])
                 t = timeit(lambda: spmm(csr, X, r0, r1, out=out, threshold=th, hub_threshold=hb),
                            reps)
                 nz = int((csr.row_ptr[r1] - csr.row_ptr[r0]).item())
@@ -72,16 +72,16 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--sweep", action="store_true")
-    ap.add_argument("--heavy", default="2048")
-    ap.add_argument("--hub", default="4096")
+    ap.add_argument("--heavy", default="auto")
+    ap.add_argument("--hub", default="auto")
     args = ap.parse_args()
     spec = graphs.SHAPES[args.shape]
     S = graphs.synthetic_graph(args.shape, seed=0)
     F, K, n = spec["features"], spec["hops"], S.n
     X0 = torch.from_numpy(graphs.synthetic_features(args.shape, n, F, seed=1)).cuda()
     csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device="cuda")
-    heavies = [int(x) for x in args.heavy.split(",")]
-    hubs = [int(x) for x in args.hub.split(",")]
+    heavies = [None if x == "auto" else int(x) for x in args.heavy.split(",")]
+    hubs = [None if x == "auto" else int(x) for x in args.hub.split(",")]
     if args.sweep:
         sweep(csr, X0, n, F, args.reps, heavies, hubs)
         return

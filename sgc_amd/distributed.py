@@ -155,6 +155,41 @@ class RowPartitionedPropagator:
         full.copy_(h_full)
         return None
 
+    def autotune(self, X0, K, output="sharded", candidates=(224, 304, 160), reps=2):
+        """Pick group_floats by timing whole propagations (collective: every
+        rank must call it with the same arguments).  The best grouping depends
+        on the exchange rate, which only the node knows: with a fast all-gather
+        the hop after it is compute-bound and fewer, wider groups (cheaper
+        launches) win; with a slow one more groups hide more of it
+        (DESIGN.md 6).  Each candidate's time is the max over ranks, so every
+        rank picks the same width (the all-gathers' shapes must agree).
+        Returns {group_floats: seconds per propagation}."""
+        import time
+
+        def sync():
+            if X0.is_cuda:
+                torch.cuda.synchronize(X0.device)
+            dist.barrier(group=self.group)
+
+        on_dev = X0.is_cuda and dist.get_backend(self.group) == "nccl"
+        times = {}
+        for gf in candidates:
+            self.group_floats = max(2, int(gf) // 2 * 2)
+            self._bufs.clear()
+            self.propagate(X0, K, output=output)  # warm-up: buffers, plans
+            sync()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                self.propagate(X0, K, output=output)
+            sync()
+            t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64,
+                             device=X0.device if on_dev else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            times[self.group_floats] = float(t.item())
+        self.group_floats = min(times, key=lambda g: (times[g], g))
+        self._bufs.clear()
+        return times
+
     def propagate(self, X0, K, out=None, output="replicated"):
         """output="replicated": the full X_K [N, F] on every rank (one more
         all-gather after the last hop).  output="sharded": this rank's rows

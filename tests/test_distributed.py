@@ -52,7 +52,7 @@ def _oracle_spmm(shard, X, out):
 
 
 def _worker(rank, world, port, case, K, result_q, group_floats=128, staging=False,
-            output="replicated"):
+            output="replicated", autotune=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -63,8 +63,13 @@ def _worker(rank, world, port, case, K, result_q, group_floats=128, staging=Fals
         prop = RowPartitionedPropagator(shard, spmm_fn=_oracle_spmm, group_floats=group_floats,
                                         host_staging=staging)
         X0 = torch.from_numpy(case["X"])
+        tuned = None
+        if autotune:
+            times = prop.autotune(X0, K, output=output, candidates=(8, 64, 16), reps=1)
+            assert sorted(times) == [8, 16, 64] and prop.group_floats in times
+            tuned = prop.group_floats
         out = prop.propagate(X0, K, output=output)
-        result_q.put((rank, out.numpy()))
+        result_q.put((rank, out.numpy()) if not autotune else (rank, (out.numpy(), tuned)))
     finally:
         dist.destroy_process_group()
 
@@ -98,6 +103,27 @@ def test_row_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, gf, st
         p.join(timeout=60)
         assert p.exitcode == 0
     _check_results(results, case, K, world, output, name)
+
+
+@pytest.mark.parametrize("output", ["sharded", "replicated"])
+def test_row_partition_autotune_gloo(tiny_cases, oracle, output):
+    """autotune() times each group width collectively: every rank must pick
+    the same width (the all-gathers' shapes depend on it) and the result stays
+    bit-exact."""
+    case, K, world = tiny_cases["norm_n48_F65"], 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, K, q, 128, False, output,
+                                               True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len({got[r][1] for r in range(world)}) == 1
+    _check_results({r: got[r][0] for r in range(world)}, case, K, world, output, "autotune")
 
 
 # ---------------------------------------------------------------------------
