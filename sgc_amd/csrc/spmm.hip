@@ -324,15 +324,25 @@ constexpr int kHubLoaders = 15;
 constexpr int kHubInstr = 16;  // consecutive nonzeros per loader lane per round
 constexpr int kHubDepth = 3;   // rounds held in loader registers (17 loads each: vmcnt <= 63)
 constexpr int kHubUnroll = 6;  // lcm(kHubDepth, 2): X ring slot and colv parity compile-time
+#ifndef SGC_HUB_PRE
+#define SGC_HUB_PRE 3
+#endif
+constexpr int kHubPre = SGC_HUB_PRE;  // LDS batches of 4 nonzeros the chain reads ahead
+#ifndef SGC_HUB_SCHED
+#define SGC_HUB_SCHED 0
+#endif
 
 template <int HC>
 struct HubShape {
     static constexpr int kSegs = kWave / HC;                     // nonzero runs per loader wave
     static constexpr int kPerLoader = kHubInstr * kSegs;         // nonzeros per loader per round
     static constexpr int kRound = kHubLoaders * kPerLoader;      // nonzeros per round (240 / 480)
-    // dwords per gxT row: 4 mod 64 (conflict-free b128), and >= kRound + 12 for
-    // the FMA loop's read-ahead (3 batches of 4 past the last full batch)
-    static constexpr int kStride = (kRound + 12 + 63) / 64 * 64 + 4;
+    // chain read-ahead in batches of 4; HC = 64 fits at most 4 in 160 KB of LDS
+    static constexpr int kPre = (HC == 64 && kHubPre > 4) ? 4 : kHubPre;
+    static constexpr int kPad = 4 * kPre;                        // read-ahead past kRound
+    // dwords per gxT row: 4 mod 64 (conflict-free b128), and >= kRound + kPad
+    // for the FMA loop's read-ahead (kHubPre batches of 4 past the last full batch)
+    static constexpr int kStride = (kRound + kPad + 63) / 64 * 64 + 4;
 };
 
 template <int HC>
@@ -343,7 +353,7 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
     using Sh = HubShape<HC>;
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) float gxT[2][HC * Sh::kStride];  // 2 x 66.5 KB
-    __shared__ __attribute__((aligned(16))) float gv[2][Sh::kRound + 12];  // + read-ahead
+    __shared__ __attribute__((aligned(16))) float gv[2][Sh::kRound + Sh::kPad];  // + read-ahead
     const int lane = threadIdx.x & (kWave - 1);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
     const int h = blockIdx.x / n_chunks;
@@ -432,7 +442,47 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
                 // chain (a ds_read's ~64-cycle latency otherwise lands on the
                 // chain every four FMAs); reads past n stay inside the padded
                 // row / value buffers (kStride, gv) and are never used.
-                constexpr int kPre = 3;
+                constexpr int kPre = Sh::kPre;
+#if SGC_HUB_SCHED
+                // Ring of 2*kPre slots with compile-time indices: batch b sits
+                // in slot b mod 2kPre, loaded kPre batches before its FMAs, so
+                // no register is copied (a copied load result makes the wave
+                // wait for it) and a sched_barrier keeps each read where it is
+                // issued (left alone, the scheduler sinks it to one batch
+                // before its use and the chain waits on LDS latency).
+                constexpr int kR = 2 * kPre;
+                f4 xr[kR], vr[kR];
+#pragma unroll
+                for (int i = 0; i < kPre; ++i) {
+                    xr[i] = xs[i];
+                    vr[i] = vs[i];
+                }
+                int q = 0;
+                for (; q + kR <= n4; q += kR) {
+#pragma unroll
+                    for (int i = 0; i < kR; ++i) {
+                        const int s = (i + kPre) % kR;
+                        xr[s] = xs[q + i + kPre];
+                        vr[s] = vs[q + i + kPre];
+                        __builtin_amdgcn_sched_barrier(0);
+                        acc = __builtin_fmaf(vr[i][0], xr[i][0], acc);
+                        acc = __builtin_fmaf(vr[i][1], xr[i][1], acc);
+                        acc = __builtin_fmaf(vr[i][2], xr[i][2], acc);
+                        acc = __builtin_fmaf(vr[i][3], xr[i][3], acc);
+                    }
+                }
+                // tail: batches q .. n4-1 (< kR); the first kPre are in slots
+#pragma unroll
+                for (int j = 0; j < kR; ++j)
+                    if (q + j < n4) {
+                        const f4 x = j < kPre ? xr[j] : xs[q + j];
+                        const f4 v = j < kPre ? vr[j] : vs[q + j];
+                        acc = __builtin_fmaf(v[0], x[0], acc);
+                        acc = __builtin_fmaf(v[1], x[1], acc);
+                        acc = __builtin_fmaf(v[2], x[2], acc);
+                        acc = __builtin_fmaf(v[3], x[3], acc);
+                    }
+#else
                 f4 xq[kPre], vq[kPre];
 #pragma unroll
                 for (int i = 0; i < kPre; ++i) {
@@ -460,6 +510,7 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
                         acc = __builtin_fmaf(vq[i][2], xq[i][2], acc);
                         acc = __builtin_fmaf(vq[i][3], xq[i][3], acc);
                     }
+#endif
                 const float *xt = &gxT[buf][fl * Sh::kStride];
                 for (int kk = n4 * 4; kk < n; ++kk) acc = __builtin_fmaf(gv[buf][kk], xt[kk], acc);
             }
