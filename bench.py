@@ -11,26 +11,34 @@ A "step" = one full K-hop propagation.  N > 1 (sgc_amd.distributed), total
 work fixed, so scaling is "strong":
   --partition rows (default)  S row-partitioned (equal-row blocks, SURVEY.md
                 8(e)); RCCL all-gather of X_k after each hop that feeds another,
-                pipelined in 128-float feature groups
+                pipelined in feature groups
   --partition features  each rank runs all K hops on its block of feature
                 columns over the full S, no exchange between hops
-  --output sharded (default)  each rank ends with its row block of X_K -- the
-                layout the data-parallel classifier consumes
-                (sgc_amd.distributed.ShardedSGCTrainer); no gather after the
-                last hop (rows) / one all-to-all (features)
+  --output sharded (default)  each rank ends with its row block of X_K
   --output replicated  every rank ends with all of X_K (one more all-gather)
 The other output mode is timed too (`alt_output`, --alt-steps).
 
-Also printed (same JSON line):
-  roofline      dominant kernel (the CSR SpMM) -- algorithmic bytes per hop
-                (gather model: 4(N+1) + 8nnz + 4F nnz + 4F N) / the kernel's
-                mean duration measured with events on the launch stream;
-                `traffic` = HBM bytes per launch from rocprofv3 PMC counters
-                when profiles/pmc_<shape>.json exists (else null)
+Also printed (same JSON line, N = 1):
+  roofline      the SpMM hop (spmm_csr_kernel, joined with spmm_hub_kernel on
+                its side stream), timed live with HIP events on the launch
+                stream, each kernel also timed on its own stream
+                (sgc_timing_*).  achieved = MEASURED bytes per launch
+                (rocprofv3 FETCH_SIZE + WRITE_SIZE, calibrated, from
+                profiles/pmc_<shape>.json -- used only when its recorded
+                libsgc_amd.so sha256 equals the library being timed) / the
+                mean hop time; frac = achieved / 8 TB/s.  Beside it the two
+                byte MODELS of SURVEY.md 8(d): the gather model (every
+                nonzero re-reads its X row; no cache reuse; an upper bound
+                that exceeds the HBM peak when the live X slice is
+                cache-resident) and the compulsory model (S, X and Y once).
+  shapes        the same measurement for the other BASELINE configs
+                (Cora-, Pubmed-, RMAT-shape), rank 0 at N = 1
   cpu_baseline  the reference's arithmetic as written -- torch.spmm(COO, X)
-                (utils.py:95) on this host's CPU, one hop, rank 0 at N = 1
+                (utils.py:95), median of 3 hops on this host; plus torch CSR
+                and this library's own CPU twin at every available core
 """
 import argparse
+import hashlib
 import json
 import os
 import platform
@@ -45,15 +53,32 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from sgc_amd import graphs  # noqa: E402
-from sgc_amd.propagate import DeviceCSR, propagate  # noqa: E402
+from sgc_amd.propagate import (DeviceCSR, collect_kernel_timing, kernel_timing,  # noqa: E402
+                               propagate)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BASELINE_METRIC = ("propagated edges/sec (K-hop SpMM) + precompute wall-time, "
                    "Reddit K=2 at 1/2/4/8 GPUs")
+SUB_STEPS = {"cora": (20, 5), "pubmed": (20, 5), "reddit": (10, 3), "rmat": (3, 1)}
 
 
-def algorithmic_bytes_per_hop(n, nnz, F):
+def gather_model_bytes(n, nnz, F):
+    """row_ptr + (col, val) + one X row per nonzero + Y."""
     return 4 * (n + 1) + 8 * nnz + 4 * F * nnz + 4 * F * n
+
+
+def compulsory_bytes(n, nnz, F):
+    """S once, X once, Y once."""
+    return 4 * (n + 1) + 8 * nnz + 8 * F * n
+
+
+def lib_sha256():
+    from sgc_amd import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
 
 
 def cpu_model():
@@ -67,51 +92,257 @@ def cpu_model():
     return platform.processor()
 
 
-def cpu_baseline(S, X_host, budget_s=30.0):
+def host_cores():
+    """(cores this process may use, how that was decided): the affinity mask,
+    bounded by a cgroup CPU quota when one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    how = f"sched_getaffinity={n}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) / int(period)))
+            how += f", cgroup cpu.max quota={q}"
+            n = min(n, q)
+    except (OSError, ValueError):
+        pass
+    return max(1, n), how
+
+
+def cpu_baseline(S, X_host, reps=3):
     """The reference's arithmetic on this host: torch.spmm(COO, X) -- what
-    utils.py:95 runs each hop.  One hop over the full graph after a warm-up
+    utils.py:95 runs each hop -- median of `reps` full hops after a warm-up
     hop on 64 feature columns (allocator first touch).  aten's COO kernel is
     single-threaded whatever torch.get_num_threads() says, so
-    cores = 1.  Also times the CSR variant at all threads (bit-identical
-    output, the best CPU torch path) when the budget allows."""
+    cores = 1.  Beside it, at every available core: torch CSR
+    (torch.sparse.mm, bit-identical output, the best CPU torch path) and this
+    library's own CPU twin (sgc_propagate_f32_cpu, bit-identical)."""
+    from sgc_amd.propagate import DeviceCSR as _CSR
+    from sgc_amd.propagate import propagate as _prop
     rows, cols, vals = S.coo()
     adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([rows, cols])),
                                   torch.from_numpy(vals), (S.n, S.n))
     X = torch.from_numpy(X_host)
     torch.spmm(adj, X[:, :64].contiguous())
-    t0 = time.perf_counter()
-    torch.spmm(adj, X)
-    t_coo = time.perf_counter() - t0
-    rec = {"value": S.nnz / t_coo, "unit": "edges/s", "cores": 1, "kind": "reference",
-           "sample": f"1 hop of torch.spmm(COO fp32 {S.n}x{S.n}, nnz {S.nnz}; X [{S.n},{X.shape[1]}]) "
-                     f"on the host CPU = reference utils.py:95 as written, after a 64-column "
-                     f"warm-up; {t_coo:.2f} s",
+    t_coo = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        torch.spmm(adj, X)
+        t_coo.append(time.perf_counter() - t0)
+    med = float(np.median(t_coo))
+    cores, how = host_cores()
+    rec = {"value": S.nnz / med, "unit": "edges/s", "cores": 1, "kind": "reference",
+           "sample": f"1 hop of torch.spmm(COO fp32 {S.n}x{S.n}, nnz {S.nnz}; X [{S.n},"
+                     f"{X.shape[1]}]) = reference utils.py:95 as written; median of {reps} hops "
+                     f"after a 64-column warm-up: {med:.2f} s (aten's COO kernel is single-"
+                     f"threaded)",
+           "coo_seconds": [round(t, 3) for t in t_coo],
            "host_cpu": cpu_model(), "os_cpu_count": os.cpu_count(),
-           "torch_threads": torch.get_num_threads()}
-    if t_coo < budget_s / 3:
+           "host_cores_available": cores, "host_cores_rule": how}
+    saved = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    try:
         csr = adj.to_sparse_csr()
         torch.sparse.mm(csr, X)
-        t0 = time.perf_counter()
-        torch.sparse.mm(csr, X)
-        t_csr = time.perf_counter() - t0
-        rec["csr_all_threads"] = {"value": S.nnz / t_csr, "unit": "edges/s",
-                                  "cores": torch.get_num_threads(), "seconds": round(t_csr, 3)}
+        t_csr = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            torch.sparse.mm(csr, X)
+            t_csr.append(time.perf_counter() - t0)
+        m = float(np.median(t_csr))
+        rec["csr_all_cores"] = {"value": S.nnz / m, "unit": "edges/s", "cores": cores,
+                                "seconds_median": round(m, 4),
+                                "what": "torch.sparse.mm(adj.to_sparse_csr(), X), one hop"}
+        hc = _CSR._from_torch_cpu(adj)
+        out = torch.empty_like(X)
+        _prop(hc, X, 1, out=out)
+        t_tw = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            _prop(hc, X, 1, out=out)
+            t_tw.append(time.perf_counter() - t0)
+        m = float(np.median(t_tw))
+        rec["cpu_twin_all_cores"] = {"value": S.nnz / m, "unit": "edges/s", "cores": cores,
+                                     "seconds_median": round(m, 4),
+                                     "what": "this library's CPU twin sgc_propagate_f32_cpu, "
+                                             "one hop (bit-identical to the reference)"}
+    finally:
+        torch.set_num_threads(saved)
     return rec
 
 
-def load_traffic(shape):
+def load_traffic(shape, lib_sha):
+    """Measured bytes per hop from profiles/pmc_<shape>.json, or (None, why)
+    when absent or taken on a different build of the library."""
     p = os.path.join(ROOT, "profiles", f"pmc_{shape}.json")
     if not os.path.exists(p):
-        return None, None
+        return None, f"no {os.path.relpath(p, ROOT)}"
     with open(p) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+    if d.get("lib_sha256") != lib_sha:
+        return None, (f"{os.path.relpath(p, ROOT)} was taken on libsgc_amd.so "
+                      f"{str(d.get('lib_sha256'))[:12]}, not the timed {lib_sha[:12]}: refused")
+    return d, os.path.relpath(p, ROOT)
 
 
-def build_step(args, S, X0, dev, rank, world, distributed, K, output, timing):
-    """(step, parallelism, launch description) for one output mode.  timing =
-    {"on", "starts", "ends", "bytes"}: every SpMM launch is bracketed by HIP
-    events on its stream while timing["on"]."""
+def roofline(shape, n, nnz, F, hop_ms, light_ms, hub_ms, lib_sha, launch_desc):
+    gm = gather_model_bytes(n, nnz, F)
+    cb = compulsory_bytes(n, nnz, F)
+    t = hop_ms * 1e-3
+    pmc, src = load_traffic(shape, lib_sha)
+    rec = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "kernel": "spmm_csr_kernel (+ spmm_hub_kernel on its side stream, joined)",
+           "kernel_mean_ms": hop_ms, "launch_unit": launch_desc,
+           "light_kernel_mean_ms": light_ms, "hub_kernel_mean_ms": hub_ms,
+           "hub_tail_ms": (max(0.0, hub_ms - light_ms) if hub_ms is not None and light_ms
+                           else None),
+           "gather_model_bytes_per_launch": gm,
+           "gather_model_frac": gm / t / 1e9 / HBM_PEAK_GBS,
+           "compulsory_bytes_per_launch": cb,
+           "compulsory_frac": cb / t / 1e9 / HBM_PEAK_GBS,
+           "traffic_source": src}
+    if pmc is not None:
+        traffic = pmc["hbm_bytes_per_launch"]
+        rec.update({"achieved": traffic / t / 1e9, "frac": traffic / t / 1e9 / HBM_PEAK_GBS,
+                    "traffic": traffic, "achieved_basis": "measured (PMC FETCH_SIZE+WRITE_SIZE, "
+                    "calibrated; counts Infinity-Cache hits, so an upper bound on HBM bytes)",
+                    "l2_hit_rate": pmc.get("l2_hit_rate"),
+                    "pmc_kernel_ms": pmc.get("kernel_ms")})
+    else:
+        rec.update({"achieved": cb / t / 1e9, "frac": cb / t / 1e9 / HBM_PEAK_GBS,
+                    "traffic": None, "achieved_basis": "compulsory bytes (no matching PMC file)"})
+    return rec
+
+
+class HopTimer:
+    """hop_hook for propagate(): events around each hop on the launch stream
+    (the interval joins the hub kernel), plus the library's per-kernel events."""
+
+    def __init__(self):
+        self.on = False
+        self.pairs = []
+        self._s = None
+
+    def __call__(self, phase, h):
+        if not self.on:
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        if phase == "start":
+            self._s = ev
+        else:
+            self.pairs.append((self._s, ev))
+
+    def start(self):
+        self.pairs = []
+        collect_kernel_timing()  # drop anything recorded before
+        kernel_timing(True)
+        self.on = True
+
+    def stop(self):
+        self.on = False
+        kernel_timing(False)
+        torch.cuda.synchronize()
+        hops = [s.elapsed_time(e) for s, e in self.pairs]
+        light, hub = collect_kernel_timing()
+        return hops, light, [h for h in hub if h is not None]
+
+
+def mean_or_none(v):
+    return float(np.mean(v)) if v else None
+
+
+def timed(step, steps, warmup, distributed, dev, on_start=None, on_stop=None):
+    """W untimed warm-ups, then exactly `steps` steps between
+    synchronise + barrier pairs; returns (max-over-ranks elapsed s, per-step
+    ms from events on the current stream)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if on_start:
+        on_start()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    t0 = time.perf_counter()
+    for s, e in evs:
+        s.record()
+        step()
+        e.record()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    extra = on_stop() if on_stop else None
+    step_ms = [s.elapsed_time(e) for s, e in evs]
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    return elapsed, step_ms, extra
+
+
+def single_gpu_shape(shape, args, dev, lib_sha, steps, warmup, S=None, X_host=None, K=None):
+    """One BASELINE config on one GPU through the product path (propagate,
+    the engine under sgc_precompute): throughput, per-kernel times, roofline
+    and the first-call (ingest + plan + propagation) time."""
+    from sgc_amd.utils import sgc_precompute
+    spec = graphs.SHAPES[shape]
+    K = K or spec["hops"]
+    t_gen = time.perf_counter()
+    if S is None:
+        S = graphs.synthetic_graph(shape, seed=args.seed)
+        X_host = graphs.synthetic_features(shape, S.n, spec["features"], seed=args.seed + 1)
+    t_gen = time.perf_counter() - t_gen
+    n, F, nnz = S.n, X_host.shape[1], S.nnz
+    X0 = torch.from_numpy(X_host).to(dev)
+    # first call on a fresh torch COO adjacency (reference layout, utils.py:23-30):
+    # ingest (COO -> CSR) + plan + K hops, as sgc_precompute's first call pays it
+    rows, cols, vals = S.coo()
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([rows, cols])),
+                                  torch.from_numpy(vals), (n, n)).to(dev)
+    del rows, cols, vals
+    torch.cuda.synchronize()
+    _, first_s = sgc_precompute(X0, adj, K)
+    ingest_s = adj._sgc_amd_csr[1].ingest_seconds
+    csr = adj._sgc_amd_csr[1]
+    del adj
+    csr.plan(0, n, args.threshold, args.hub_threshold, F)
+    out_buf = torch.empty((n, F), device=dev)
+    hops = HopTimer()
+
+    def step():  # the product path of sgc_precompute (sgc_amd.propagate)
+        return propagate(csr, X0, K, out=out_buf, threshold=args.threshold, hop_hook=hops,
+                         hub_threshold=args.hub_threshold)
+
+    elapsed, step_ms, (hop_ms, light, hub) = timed(step, steps, warmup, False, dev,
+                                                   on_start=hops.start, on_stop=hops.stop)
+    hop_mean = float(np.mean(hop_ms))
+    rec = {"value": K * nnz * steps / elapsed, "unit": "edges/s",
+           "ms_per_step": elapsed * 1e3 / steps,
+           "ms_per_step_median": float(np.median(step_ms)),
+           "ms_per_step_events": [round(v, 4) for v in step_ms],
+           "steps": steps, "warmup": warmup,
+           "config": {"workload": f"{shape}-shape sgc_precompute K={K}", "nodes": n,
+                      "undirected_edges": spec["edges"], "nnz": nnz, "features": F, "hops": K},
+           "first_call_seconds": round(first_s, 4), "ingest_seconds": round(ingest_s, 4),
+           "generate_seconds": round(t_gen, 2),
+           "roofline": roofline(shape, n, nnz, F, hop_mean, mean_or_none(light),
+                                mean_or_none(hub), lib_sha, f"one hop over all {n} rows"),
+           "hop_ms_median": float(np.median(hop_ms))}
+    del X0, out_buf, csr
+    torch.cuda.empty_cache()
+    return rec, S, X_host
+
+
+def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
+    """(step, parallelism, launch description) for the N > 1 path.  While
+    timing["on"], every SpMM launch is bracketed by events on its stream and
+    its compulsory bytes (its rows of S, the X columns it reads once, its Y)
+    are recorded."""
     n, F = X0.shape
 
     def bracket(fn, nbytes):
@@ -122,35 +353,10 @@ def build_step(args, S, X0, dev, rank, world, distributed, K, output, timing):
             s.record()
             r = fn(*a, **k)
             e.record()
-            timing["starts"].append(s)
-            timing["ends"].append(e)
+            timing["pairs"].append((s, e))
             timing["bytes"].append(nbytes(*a))
             return r
         return run
-
-    if not distributed:
-        csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
-        csr.plan(0, n, args.threshold, args.hub_threshold, F)
-        out_buf = torch.empty((n, F), device=dev)
-        ev = {}
-
-        def hook(phase, h):
-            if not timing["on"]:
-                return
-            if phase == "start":
-                ev["s"] = torch.cuda.Event(enable_timing=True)
-                ev["s"].record()
-            else:
-                e = torch.cuda.Event(enable_timing=True)
-                e.record()
-                timing["starts"].append(ev["s"])
-                timing["ends"].append(e)
-                timing["bytes"].append(algorithmic_bytes_per_hop(n, S.nnz, F))
-
-        def step():  # the product path of sgc_precompute (sgc_amd.propagate)
-            return propagate(csr, X0, K, out=out_buf, threshold=args.threshold, hop_hook=hook,
-                             hub_threshold=args.hub_threshold)
-        return step, "single-gpu", f"one hop over all {n} rows"
 
     backend = "rccl" if args.dist_backend == "nccl" else "gloo rehearsal"
     staging = args.dist_backend == "gloo"
@@ -162,28 +368,27 @@ def build_step(args, S, X0, dev, rank, world, distributed, K, output, timing):
 
         def launch_bytes(X, r0, r1, out):
             nz, w = int(rp[r1] - rp[r0]), X.shape[1]
-            return 4 * (r1 - r0 + 1) + 8 * nz + 4 * w * nz + 4 * w * (r1 - r0)
+            return 4 * (r1 - r0 + 1) + 8 * nz + 4 * w * n + 4 * w * (r1 - r0)
 
-        spmm_fn = bracket(lambda X, r0, r1, out: spmm_hip(
-            csr, X, r0, r1, out=out, threshold=args.threshold,
-            hub_threshold=args.hub_threshold), launch_bytes)
-        prop = FeaturePartitionedPropagator(csr, rank=rank, world_size=world, spmm_fn=spmm_fn,
-                                            chunks=args.chunks, host_staging=staging)
+        prop = FeaturePartitionedPropagator(
+            csr, rank=rank, world_size=world,
+            spmm_fn=bracket(lambda X, r0, r1, out: spmm_hip(
+                csr, X, r0, r1, out=out, threshold=args.threshold,
+                hub_threshold=args.hub_threshold), launch_bytes),
+            chunks=args.chunks, host_staging=staging)
         fb, fB = feature_bounds(F, world)
         exch = ("one all-to-all of the row blocks of X_K" if output == "sharded" else
                 f"one all-gather of X_K pipelined with the last hop in {args.chunks} row chunks")
         par = (f"feature-partition x{world} ({fB}-column blocks, all K hops local) + {backend} "
                f"{exch}; output {output}")
-        unit = (f"rank 0's SpMM launches (mean): hops over all {n} rows or last-hop row blocks, "
-                f"{int(fb[1] - fb[0])} feature columns")
+        unit = f"rank 0's SpMM launches, {int(fb[1] - fb[0])} feature columns"
     else:
         from sgc_amd.distributed import RowPartitionedPropagator, _default_spmm, make_shard
         shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
-        nnz_l = shard.nnz
 
         def launch_bytes(sh, X, out):
-            fg = X.shape[1]
-            return 4 * (sh.rows + 1) + 8 * nnz_l + 4 * fg * nnz_l + 4 * fg * sh.rows
+            w = X.shape[1]
+            return 4 * (sh.rows + 1) + 8 * sh.nnz + 4 * w * n + 4 * w * sh.rows
 
         auto = args.group_floats == "auto"
         prop = RowPartitionedPropagator(shard, spmm_fn=bracket(_default_spmm, launch_bytes),
@@ -199,39 +404,12 @@ def build_step(args, S, X0, dev, rank, world, distributed, K, output, timing):
                 "all-gather of X_k after every hop")
         par = (f"row-partition x{world} (equal-row blocks) + {backend} {exch}, pipelined in "
                f"{gf}-float feature groups{tuned}; output {output}")
-        unit = (f"one hop of one {gf}-float feature group over rank 0's "
-                f"{shard.rows} rows ({nnz_l} nnz)")
-    out = None
-    if output == "replicated":
-        out = torch.empty((n, F), device=dev)
+        unit = f"rank 0's {shard.rows} rows ({shard.nnz} nnz)"
+    out = torch.empty((n, F), device=dev) if output == "replicated" else None
 
     def step():
         return prop.propagate(X0, K, out=out, output=output)
     return step, par, unit
-
-
-def timed(step, steps, warmup, distributed, dev, timing):
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    timing["on"] = True
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    timing["on"] = False
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    return elapsed
 
 
 def main():
@@ -243,6 +421,9 @@ def main():
     ap.add_argument("--hops", type=int, default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shapes", default="cora,pubmed,rmat",
+                    help="N=1: other BASELINE configs measured into the same line "
+                         "(comma list, or 'none')")
     ap.add_argument("--threshold", type=int, default=None, help="heavy-row threshold")
     ap.add_argument("--hub-threshold", type=int, default=None, help="hub-row threshold")
     ap.add_argument("--group-floats", default="auto",
@@ -265,9 +446,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
     local_dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
@@ -284,75 +464,84 @@ def main():
 
     spec = graphs.SHAPES[args.shape]
     K = args.hops or spec["hops"]
-    t_gen = time.perf_counter()
+    lib_sha = lib_sha256()
+    metric = (BASELINE_METRIC if args.shape == "reddit" and K == 2 else
+              f"propagated edges/sec (K-hop SpMM), {args.shape}-shape K={K}")
+    rec = {"metric": metric, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic (seeded R-MAT graph + AugNorm, SURVEY.md 8(d))"}
+
+    if not distributed:
+        main_rec, S, X_host = single_gpu_shape(args.shape, args, dev, lib_sha, args.steps,
+                                               args.warmup, K=K)
+        cfg = main_rec.pop("config")
+        cfg.update({"parallelism": "single-gpu", "heavy_threshold": args.threshold,
+                    "hub_threshold": args.hub_threshold})
+        rec.update({"value": main_rec.pop("value"), "ms_per_step": main_rec.pop("ms_per_step"),
+                    "config": cfg})
+        main_rec.pop("steps"), main_rec.pop("warmup"), main_rec.pop("unit")
+        rec.update(main_rec)
+        rec["precompute_seconds"] = rec["ms_per_step"] / 1e3
+        rec["lib_sha256"] = lib_sha
+        if not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(S, X_host)
+        del S, X_host
+        subs = [s for s in args.shapes.split(",") if s and s != "none" and s != args.shape]
+        if subs:
+            rec["shapes"] = {}
+            for sh in subs:
+                st, wu = SUB_STEPS[sh]
+                r, _, _ = single_gpu_shape(sh, args, dev, lib_sha, st, wu)
+                r.pop("ms_per_step_events", None)
+                rec["shapes"][sh] = r
+        print(json.dumps(rec), flush=True)
+        return
+
     S = graphs.synthetic_graph(args.shape, seed=args.seed)
     X_host = graphs.synthetic_features(args.shape, S.n, spec["features"], seed=args.seed + 1)
-    t_gen = time.perf_counter() - t_gen
     n, F, nnz = S.n, X_host.shape[1], S.nnz
     X0 = torch.from_numpy(X_host).to(dev)
-
-    timing = {"on": False, "starts": [], "ends": [], "bytes": []}
-    step, parallelism, unit_desc = build_step(args, S, X0, dev, rank, world, distributed, K,
-                                              args.output, timing)
-    elapsed = timed(step, args.steps, args.warmup, distributed, dev, timing)
-    kern_ms = [s.elapsed_time(e) for s, e in zip(timing["starts"], timing["ends"])]
-    bytes_launch = float(np.mean(timing["bytes"])) if timing["bytes"] else float("nan")
-
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = K * nnz * args.steps / elapsed
-    kern_mean_ms = float(np.mean(kern_ms)) if kern_ms else float("nan")
-    achieved = bytes_launch / (kern_mean_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(args.shape) if not distributed else (None, None)
-
+    tm = {"on": False, "pairs": [], "bytes": []}
+    step, parallelism, unit_desc = build_dist_step(args, S, X0, dev, rank, world, K, args.output,
+                                                   tm)
+    elapsed, step_ms, _ = timed(step, args.steps, args.warmup, True, dev,
+                                on_start=lambda: tm.update(on=True),
+                                on_stop=lambda: tm.update(on=False))
+    launch_ms = [s.elapsed_time(e) for s, e in tm["pairs"]]
     alt = None
-    if distributed and args.alt_steps > 0:
+    if args.alt_steps > 0:
         alt_mode = "replicated" if args.output == "sharded" else "sharded"
-        t_alt = {"on": False, "starts": [], "ends": [], "bytes": []}
-        alt_step, alt_par, _ = build_step(args, S, X0, dev, rank, world, distributed, K, alt_mode,
-                                          t_alt)
-        e_alt = timed(alt_step, args.alt_steps, 1, distributed, dev, t_alt)
+        alt_step, alt_par, _ = build_dist_step(args, S, X0, dev, rank, world, K, alt_mode,
+                                               {"on": False})
+        e_alt, _, _ = timed(alt_step, args.alt_steps, 1, True, dev)
         alt = {"output": alt_mode, "parallelism": alt_par, "steps": args.alt_steps,
                "ms_per_step": e_alt * 1e3 / args.alt_steps,
                "value": K * nnz * args.alt_steps / e_alt}
-
-    rec = None
     if rank == 0:
-        rec = {
-            "metric": (BASELINE_METRIC if args.shape == "reddit" and K == 2 else
-                       f"propagated edges/sec (K-hop SpMM), {args.shape}-shape K={K}"),
-            "value": value,
-            "unit": "edges/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (seeded R-MAT graph + AugNorm, SURVEY.md 8(d))",
-            "config": {"workload": f"{args.shape}-shape sgc_precompute K={K}", "nodes": n,
-                       "undirected_edges": spec["edges"], "nnz": nnz, "features": F, "hops": K,
-                       "parallelism": parallelism, "heavy_threshold": args.threshold,
-                       "hub_threshold": args.hub_threshold},
-            "precompute_seconds": ms_per_step / 1e3,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "spmm_csr_kernel + spmm_hub_kernel (side stream, joined)",
-                         "kernel_mean_ms": kern_mean_ms,
-                         "algorithmic_bytes_per_launch": bytes_launch,
-                         "launch_unit": unit_desc, "traffic_source": traffic_src,
-                         "compulsory_bytes_per_hop": 4 * (n + 1) + 8 * nnz + 8 * F * n},
-            "generate_seconds": round(t_gen, 2),
-        }
+        rec.update({"value": K * nnz * args.steps / elapsed,
+                    "ms_per_step": elapsed * 1e3 / args.steps,
+                    "ms_per_step_median_rank0": float(np.median(step_ms)),
+                    "config": {"workload": f"{args.shape}-shape sgc_precompute K={K}", "nodes": n,
+                               "undirected_edges": spec["edges"], "nnz": nnz, "features": F,
+                               "hops": K, "parallelism": parallelism, "launch_unit": unit_desc},
+                    "lib_sha256": lib_sha})
+        if launch_ms:
+            t_l = float(np.mean(launch_ms)) * 1e-3
+            b_l = float(np.mean(tm["bytes"]))
+            rec["roofline"] = {
+                "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "achieved": b_l / t_l / 1e9, "frac": b_l / t_l / 1e9 / HBM_PEAK_GBS,
+                "traffic": None, "achieved_basis": "compulsory bytes per launch (rank 0)",
+                "kernel": "spmm_csr_kernel (+ spmm_hub_kernel, joined), rank 0's launches",
+                "kernel_mean_ms": t_l * 1e3, "launches": len(launch_ms),
+                "compulsory_bytes_per_launch": b_l}
+        rec["precompute_seconds"] = rec["ms_per_step"] / 1e3
         if alt is not None:
             rec["alt_output"] = alt
-        if world == 1 and not distributed and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(S, X_host)
         print(json.dumps(rec), flush=True)
-    if distributed:
-        dist.barrier()
-        dist.destroy_process_group()
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

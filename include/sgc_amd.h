@@ -15,6 +15,10 @@
  *     calls documented as "synchronous";
  *   - return 0 on success, a positive SGC_E* code on failure;
  *     sgc_last_error() returns a thread-local message for the last failure;
+ *   - thread safety: every entry point may be called from several host
+ *     threads at once (on different streams); the SpMM's internal side
+ *     stream (hub rows) is serialised per device so one call's fork/join
+ *     never interleaves with another's;
  *   - indices are int32 (n_rows, n_cols, nnz < 2^31), values fp32.
  */
 #ifndef SGC_AMD_H
@@ -174,6 +178,18 @@ int sgc_spmm_csr_f32(const int32_t *row_ptr, const int32_t *col_idx, const float
                      const int32_t *plan, int64_t n_heavy, int64_t n_hub,
                      int32_t heavy_threshold, void *stream);
 
+/* Per-kernel launch timing (diagnostics; off by default).  While enabled,
+ * every sgc_spmm_csr_f32 records timing events around its light/heavy-row
+ * kernel and around its hub-row kernel, each on the stream that kernel runs
+ * on.  sgc_timing_collect waits for the recorded launches (synchronous) and
+ * writes, in launch order, light_ms_host[i] and hub_ms_host[i] (-1 when the
+ * launch had no hub rows); *n_host = launches recorded since the last
+ * collect (SGC_ENOMEM when capacity is smaller; nothing is consumed then).
+ * Do not enable while capturing a graph. */
+int sgc_timing_enable(int on);
+int sgc_timing_collect(float *light_ms_host, float *hub_ms_host, int64_t capacity,
+                       int64_t *n_host);
+
 /* K hops X_K = S^K X_0 over all n_rows rows (utils.py:92-97, the whole
  * sgc_precompute loop).  out (row stride ldo) receives X_K.  Intermediate
  * hops live in the workspace with 128-B aligned rows (ld = F rounded up to 32
@@ -215,7 +231,7 @@ int sgc_linear_f32(const float *X, int64_t ldx, const float *W, const float *b,
  *     dW   = (softmax(z) - onehot(y))^T X / M,     db = sum_m (...) / M
  * loss is one float; dW [C,K], db [C] (db may be NULL); logits [M,C] with row
  * stride ldl are written when non-NULL.  C <= 64.  Labels must lie in
- * [0, C) (not checked on the device).  Reductions run in a fixed order:
+ * [0, C) (not checked on the device; the Python layer checks them).  Reductions run in a fixed order:
  * results are bitwise reproducible run to run; within fp32 tolerance of torch.
  * workspace: sgc_linear_xent_workspace(M, K, C) bytes.
  * ------------------------------------------------------------------------- */
@@ -224,6 +240,34 @@ int sgc_linear_xent_f32(const float *X, int64_t ldx, const float *W, const float
                         const int64_t *labels, int64_t M, int64_t K, int64_t C, float *loss,
                         float *dW, float *db, float *logits, int64_t ldl, void *workspace,
                         int64_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Host (CPU) twins, for CPU tensors: the reference runs utils.py:92-97 on the
+ * CPU whenever CUDA is off (args.py:39 --no-cuda; load_citation(cuda=False)).
+ * Every pointer here is a HOST pointer; the calls are synchronous and
+ * thread-safe (no shared state).  Same numerical contract as the GPU entry
+ * points: bit-identical to torch.spmm's CPU kernel.  n_threads <= 0 = all
+ * hardware threads; threads own whole rows.
+ *
+ * sgc_coo_to_csr_cpu: as sgc_coo_to_csr (stable by row, no coalescing;
+ *   status bits 1/2/4), SGC_ERANGE on an out-of-range index.
+ * sgc_spmm_csr_f32_cpu: as sgc_spmm_csr_f32 (utils.py:95), no plan.
+ * sgc_propagate_f32_cpu: as sgc_propagate_f32 (utils.py:92-97); workspace
+ *   = sgc_propagate_cpu_workspace(n_rows, F, K) bytes of host memory.
+ * ------------------------------------------------------------------------- */
+int sgc_coo_to_csr_cpu(const int64_t *rows, const int64_t *cols, const float *vals,
+                       int64_t nnz, int64_t n_rows, int64_t n_cols,
+                       int32_t *row_ptr, int32_t *col_idx, float *val_out,
+                       uint32_t *status_host);
+int sgc_spmm_csr_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                         int64_t row_begin, int64_t row_end,
+                         const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
+                         int32_t n_threads);
+int64_t sgc_propagate_cpu_workspace(int64_t n_rows, int64_t F, int32_t K);
+int sgc_propagate_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                          int64_t n_rows, const float *X0, int64_t ldx, float *out,
+                          int64_t ldo, int64_t F, int32_t K, void *workspace,
+                          int64_t workspace_bytes, int32_t n_threads);
 
 #ifdef __cplusplus
 }

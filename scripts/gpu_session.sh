@@ -7,6 +7,11 @@ ROOTDIR=$(pwd)
 OUT=$ROOTDIR/gpurun_out
 mkdir -p "$OUT"
 STEPS=${STEPS:-"pytest smoke bench prof"}
+# progress marker for long single steps (the RMAT-shape test and bench leg
+# each run a few minutes without a new output line)
+( while sleep 45; do date +%T >> "$OUT/heartbeat.log"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 run() {
   local name=$1; shift
   local t0=$(date +%s)
@@ -32,9 +37,13 @@ for s in $STEPS; do
                 --dist-backend gloo ${DIST_ARGS} ;;
     rdist)  run rdist timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                 --master-addr 127.0.0.1 --master-port 29536 drivers/reddit_dist.py --check --test ;;
+    pmc)    for sh in ${PMC_SHAPES:-reddit rmat}; do
+              run pmc_$sh env PMC_SHAPE=$sh bash "$ROOTDIR/scripts/pmc_session.sh"
+            done ;;
     prof)   cd /tmp && export TMPDIR=/tmp && \
             run prof timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
-                --output-format csv -- python3 "$ROOTDIR/bench.py" --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS}
+                --output-format csv -- python3 "$ROOTDIR/bench.py" --steps 10 --warmup 3 --no-cpu-baseline \
+                --shapes none ${BENCH_ARGS}
             cd "$ROOTDIR" ;;
   esac
 done

@@ -1,27 +1,39 @@
-"""HBM traffic of the SpMM kernel from rocprofv3 PMC counters.
+"""Measured memory traffic of the SpMM hop from rocprofv3 PMC counters.
 
-    # on the GPU box, one counter set per pass (gfx950 TCC slots: FETCH_SIZE
-    # costs 3 of 4, WRITE_SIZE 2), kernel trace only beside the counters:
+    # on the GPU box (scripts/pmc_session.sh runs these), one counter set per
+    # pass (gfx950 TCC slots: FETCH_SIZE costs 3 of 4, WRITE_SIZE 2), kernel
+    # trace only beside the counters:
     cd /tmp && export TMPDIR=/tmp
-    rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d OUT/pmc_fetch -o p -- \
-        python3 REPO/scripts/pmc_traffic.py workload
-    rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d OUT/pmc_write -o p -- \
-        python3 REPO/scripts/pmc_traffic.py workload
-    rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d OUT/pmc_l2 -o p -- \
-        python3 REPO/scripts/pmc_traffic.py workload
-    python3 REPO/scripts/pmc_traffic.py summarize OUT      # -> profiles/pmc_reddit.json
+    rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d OUT/pmc_fetch -o p -- \\
+        python3 REPO/scripts/pmc_traffic.py workload SHAPE
+    rocprofv3 --pmc WRITE_SIZE ... -d OUT/pmc_write ...
+    rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum ... -d OUT/pmc_l2 ...
+    python3 REPO/scripts/pmc_traffic.py summarize OUT SHAPE   # -> profiles/pmc_<shape>.json
+
+The workload runs exactly what bench.py times: propagate() (K hops, X_0
+re-laid into 128-B rows, ping-pong buffers, last hop into the caller's
+[N, F] output) on the seeded BASELINE-shape graph, REPEATS times.  Every
+SpMM launch (spmm_csr_kernel + the spmm_hub_kernel dispatches of the same
+call) is one "launch"; the JSON holds the mean bytes per launch.
 
 Calibration (MI355X_MICROARCH.md, HBM section: FETCH_SIZE under-counts wide
 coalesced reads on gfx950 and other widths are uncalibrated): the workload
-first runs the SAME kernel over an identity S (N_cal rows, one nonzero each),
-which reads every X row exactly once with the kernel's own dwordx2 gathers and
-writes every Y row once -- a known byte count far beyond the 256 MiB
-Infinity Cache.  read_factor = known_read_bytes / (FETCH_SIZE*1024) of that
-launch is then applied to the Reddit-shape launches.
+first runs the SAME kernel over an identity S (N_cal rows, one nonzero each)
+at the shape's feature width and row layout, which reads every X row exactly
+once with the kernel's own gathers and writes every Y row once -- a known
+byte count far beyond the 256 MiB Infinity Cache.  read_factor =
+known_read_bytes / FETCH_SIZE bytes of that launch is then applied to the
+shape's launches.  FETCH_SIZE counts Infinity-Cache hits (the guide), so the
+result is the traffic beyond L2: an upper bound on HBM bytes.
+
+The record carries the sha256 of the libsgc_amd.so it was taken with and the
+tuning; bench.py refuses a record whose sha differs from the library it times.
 """
 import csv
 import glob
+import hashlib
 import json
+import math
 import os
 import sys
 
@@ -29,19 +41,35 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 N_CAL = 1_000_000
-F = 602
-LD = 608     # X / Y row stride as propagate() lays them out: 128-B rows
-LINES = (4 * F + 127) // 128  # 128-B lines one row's F floats touch (19)
 REPEATS = 3
+TUNING_KEYS = ("slice_floats", "max_vec", "hub_chunk", "hub_first", "hub_priority")
 
 
-def workload():
+def lib_sha():
+    from sgc_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def _meta_path(shape):
+    return os.environ.get("PMC_META", f"/tmp/pmc_meta_{shape}.json")
+
+
+def workload(shape):
     import numpy as np
     import torch
 
-    from sgc_amd import graphs
-    from sgc_amd.propagate import DeviceCSR, spmm
+    from sgc_amd import _lib, graphs
+    from sgc_amd.propagate import DeviceCSR, aligned_ld, propagate, spmm
     dev = torch.device("cuda", 0)
+    spec = graphs.SHAPES[shape]
+    F, K = spec["features"], spec["hops"]
+    LD = aligned_ld(F)
+    lib = _lib.load()
+    for key in TUNING_KEYS:
+        v = os.environ.get("SGC_PMC_" + key.upper())
+        if v is not None:
+            lib.sgc_set_tuning(key.encode(), int(v))
     # calibration: identity S, X row i read once, Y row i written once
     rp = np.arange(N_CAL + 1, dtype=np.int32)
     ci = np.arange(N_CAL, dtype=np.int32)
@@ -53,24 +81,18 @@ def workload():
         spmm(cal, Xc, out=Yc, use_plan=False)
     torch.cuda.synchronize()
     del Xc, Yc, cal
-    from sgc_amd import _lib
-    lib = _lib.load()
-    for key in ("slice_floats", "max_vec"):
-        v = os.environ.get("SGC_PMC_" + key.upper())
-        if v is not None:
-            lib.sgc_set_tuning(key.encode(), int(v))
-    S = graphs.synthetic_graph("reddit", seed=0)
-    X = torch.zeros((S.n, LD), device=dev)[:, :F]
-    X.copy_(torch.from_numpy(graphs.synthetic_features("reddit", S.n, F, seed=1)))
+    S = graphs.synthetic_graph(shape, seed=0)
+    X0 = torch.from_numpy(graphs.synthetic_features(shape, S.n, F, seed=1)).to(dev)
     csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
-    Y = torch.empty((S.n, LD), device=dev)[:, :F]
+    out = torch.empty((S.n, F), device=dev)
     for _ in range(REPEATS):
-        spmm(csr, X, out=Y)
+        propagate(csr, X0, K, out=out)
     torch.cuda.synchronize()
-    with open(os.environ.get("PMC_META", "/tmp/pmc_meta.json"), "w") as f:
-        json.dump({"n": S.n, "nnz": S.nnz, "F": F, "n_cal": N_CAL}, f)
-    print(f"pmc workload done: {S.nnz} nnz, tuning "
-          f"{ {k: lib.sgc_get_tuning(k.encode()) for k in ('slice_floats', 'max_vec')} }")
+    tuning = {k: int(lib.sgc_get_tuning(k.encode())) for k in TUNING_KEYS}
+    with open(_meta_path(shape), "w") as f:
+        json.dump({"shape": shape, "n": S.n, "nnz": S.nnz, "F": F, "K": K, "ld": LD,
+                   "n_cal": N_CAL, "lib_sha256": lib_sha(), "tuning": tuning}, f)
+    print(f"pmc workload done: {shape} {S.nnz} nnz, K={K}, tuning {tuning}")
 
 
 def _rows(d):
@@ -84,85 +106,96 @@ def _rows(d):
     return out
 
 
+def _kernel_ms(d):
+    """{dispatch_id: duration ms} from the kernel trace beside the counters."""
+    out = {}
+    for fn in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        with open(fn) as f:
+            for r in csv.DictReader(f):
+                try:
+                    out[int(r["Dispatch_Id"])] = (int(r["End_Timestamp"]) -
+                                                  int(r["Start_Timestamp"])) * 1e-6
+                except (KeyError, ValueError):
+                    pass
+    return out
+
+
 def _per_dispatch(rows, counter):
-    """{dispatch_id: (kernel_name, grid_size, value)} summed over dimensions."""
+    """{dispatch_id: (kernel_name, value)} summed over dimensions."""
     acc = {}
     for r in rows:
         if r.get("Counter_Name") != counter:
             continue
         k = int(r["Dispatch_Id"])
-        name = r.get("Kernel_Name", "")
-        grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
         v = float(r["Counter_Value"])
-        if k in acc:
-            acc[k] = (name, grid, acc[k][2] + v)
-        else:
-            acc[k] = (name, grid, v)
+        name = r.get("Kernel_Name", "")
+        acc[k] = (name, acc[k][1] + v) if k in acc else (name, v)
     return acc
 
 
-def summarize(out_dir):
-    n_cal, F_ = N_CAL, F
-    tag = os.environ.get("SGC_PMC_TAG", "")
-    fetch = _per_dispatch(_rows(os.path.join(out_dir, "pmc_fetch" + tag)), "FETCH_SIZE")
-    write = _per_dispatch(_rows(os.path.join(out_dir, "pmc_write" + tag)), "WRITE_SIZE")
-    l2 = _rows(os.path.join(out_dir, "pmc_l2" + tag))
+def _launches(d, K):
+    """(calibration dispatch ids, [[main id, hub ids...] per shape launch])."""
+    ks = sorted(k for k, (nm, _) in d.items() if "spmm_csr_kernel" in nm)
+    hubs = sorted(k for k, (nm, _) in d.items() if "spmm_hub_kernel" in nm)
+    cal, main = ks[:REPEATS], ks[REPEATS:REPEATS + REPEATS * K]
+    prev = [cal[-1]] + main[:-1]
+    return cal, [[k] + [h for h in hubs if p < h < k] for p, k in zip(prev, main)]
+
+
+def summarize(out_dir, shape):
+    meta = json.load(open(_meta_path(shape)))
+    K, F, LD, n_cal = meta["K"], meta["F"], meta["ld"], meta["n_cal"]
+    n, nnz = meta["n"], meta["nnz"]
+    fetch = _per_dispatch(_rows(os.path.join(out_dir, "pmc_fetch")), "FETCH_SIZE")
+    write = _per_dispatch(_rows(os.path.join(out_dir, "pmc_write")), "WRITE_SIZE")
+    l2 = _rows(os.path.join(out_dir, "pmc_l2"))
     hit, miss = _per_dispatch(l2, "TCC_HIT_sum"), _per_dispatch(l2, "TCC_MISS_sum")
+    cal_f, red_f = _launches(fetch, K)
+    cal_w, red_w = _launches(write, K)
+    _, red_h = _launches(hit, K)
 
-    def spmm_dispatches(d):
-        """(calibration launches, Reddit-shape launches): main-kernel dispatch
-        ids, each Reddit launch paired with the hub-kernel dispatches of the
-        same sgc_spmm call (the hub rows' kernel runs beside the main one)."""
-        ks = sorted(k for k, (nm, _, _) in d.items() if "spmm_csr_kernel" in nm)
-        hubs = sorted(k for k, (nm, _, _) in d.items() if "spmm_hub_kernel" in nm)
-        red = ks[REPEATS:2 * REPEATS]
-        return ks[:REPEATS], [[k] + [h for h in hubs if prev < h < k]
-                              for prev, k in zip([ks[REPEATS - 1]] + red[:-1], red)]
-
-    cal_f, red_f = spmm_dispatches(fetch)
-    cal_w, red_w = spmm_dispatches(write)
-    cal_h, red_h = spmm_dispatches(hit)
-
-    def mean(d, ks):  # ks: dispatch ids, or groups of ids summed per launch
-        vals = [sum(d[j][2] for j in k) if isinstance(k, list) else d[k][2] for k in ks]
+    def mean(d, ks):
+        vals = [sum(d[j][1] for j in k) if isinstance(k, list) else d[k][1] for k in ks]
         return sum(vals) / max(1, len(vals))
-    # line-granular: every X row touched once (LINES whole 128-B lines of its
-    # 128-B aligned LD-float row), every Y row written once, plus the CSR
-    known_read = 128 * LINES * n_cal + 4 * (n_cal + 1) + 8 * n_cal
-    known_write = 128 * LINES * n_cal
+    lines = (4 * F + 127) // 128  # 128-B lines one row's F floats touch (aligned rows)
+    known_read = 128 * lines * n_cal + 4 * (n_cal + 1) + 8 * n_cal
+    known_write = 128 * lines * n_cal
     cal_fetch_b = mean(fetch, cal_f) * 1024
     cal_write_b = mean(write, cal_w) * 1024
     read_factor = known_read / cal_fetch_b
     write_factor = known_write / cal_write_b
     red_fetch_b = mean(fetch, red_f) * 1024 * read_factor
     red_write_b = mean(write, red_w) * 1024 * write_factor
-    import math
     h, m = mean(hit, red_h), mean(miss, red_h)
-    meta = {}
-    try:
-        meta = json.load(open(os.environ.get("PMC_META", "/tmp/pmc_meta.json")))
-    except OSError:
-        pass
-    n, nnz = meta.get("n", 232965), meta.get("nnz", 23446803)
-    alg = 4 * (n + 1) + 8 * nnz + 4 * F_ * nnz + 4 * F_ * n
+    kms = _kernel_ms(os.path.join(out_dir, "pmc_fetch"))
+    main_ms = [kms[g[0]] for g in red_f if g[0] in kms]
+    alg = 4 * (n + 1) + 8 * nnz + 4 * F * nnz + 4 * F * n
+    comp = 4 * (n + 1) + 8 * nnz + 8 * F * n
     rec = {
-        "workload": "reddit-shape spmm hop (232,965 rows, 23,446,803 nnz, F=602, X/Y ld 608 "
-                    "as propagate() lays them out)",
+        "workload": f"{shape}-shape propagate() K={K} ({n} rows, {nnz} nnz, F={F}; X_0 re-laid "
+                    f"to ld {LD}, intermediates ld {LD}, last hop into ld {F}), {REPEATS} times; "
+                    f"one launch = one hop (spmm_csr_kernel + its spmm_hub_kernel dispatches)",
+        "lib_sha256": meta["lib_sha256"], "tuning": meta["tuning"],
         "hbm_bytes_per_launch": red_fetch_b + red_write_b,
         "hbm_read_bytes_per_launch": red_fetch_b,
         "hbm_write_bytes_per_launch": red_write_b,
         "raw_FETCH_SIZE_kB": mean(fetch, red_f), "raw_WRITE_SIZE_kB": mean(write, red_w),
-        "calibration": {"kernel": "same spmm kernel over identity S, ld 608", "rows": n_cal,
-                        "known_read_bytes": known_read, "known_write_bytes": known_write,
-                        "FETCH_SIZE_bytes": cal_fetch_b, "WRITE_SIZE_bytes": cal_write_b,
-                        "read_factor": read_factor, "write_factor": write_factor},
+        "calibration": {"kernel": f"same spmm kernel over identity S, F={F}, ld {LD}",
+                        "rows": n_cal, "known_read_bytes": known_read,
+                        "known_write_bytes": known_write, "FETCH_SIZE_bytes": cal_fetch_b,
+                        "WRITE_SIZE_bytes": cal_write_b, "read_factor": read_factor,
+                        "write_factor": write_factor},
         "l2_hit_rate": h / (h + m) if (h + m) > 0 and not math.isnan(h) else None,
+        "kernel_ms": (sum(main_ms) / len(main_ms)) if main_ms else None,
+        "kernel_ms_note": "spmm_csr_kernel mean duration in the profiled FETCH_SIZE pass "
+                          "(profiled passes run slower than unprofiled ones)",
         "algorithmic_bytes_per_launch": alg,
-        "compulsory_bytes_per_launch": 4 * (n + 1) + 8 * nnz + 8 * F_ * n,
+        "compulsory_bytes_per_launch": comp,
         "traffic_over_algorithmic": (red_fetch_b + red_write_b) / alg,
+        "traffic_over_compulsory": (red_fetch_b + red_write_b) / comp,
+        "launches": len(red_f),
     }
-    rec["tuning"] = {k: os.environ.get("SGC_PMC_" + k.upper()) for k in ("slice_floats", "max_vec")}
-    dst = os.path.join(ROOT, "profiles", f"pmc_reddit{tag}.json")
+    dst = os.path.join(ROOT, "profiles", f"pmc_{shape}.json")
     with open(dst, "w") as f:
         json.dump(rec, f, indent=1)
     print(json.dumps(rec, indent=1))
@@ -170,6 +203,6 @@ def summarize(out_dir):
 
 if __name__ == "__main__":
     if sys.argv[1] == "workload":
-        workload()
+        workload(sys.argv[2] if len(sys.argv) > 2 else "reddit")
     else:
-        summarize(sys.argv[2])
+        summarize(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "reddit")

@@ -52,6 +52,15 @@ SIGNATURES = {
     "sgc_linear_xent_workspace": (_i64, [_i64, _i64, _i64]),
     "sgc_linear_xent_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _p, _p, _p,
                                            _p, _i64, _p, _i64, _p]),
+    "sgc_timing_enable": (ctypes.c_int, [ctypes.c_int]),
+    "sgc_timing_collect": (ctypes.c_int, [_p, _p, _i64, ctypes.POINTER(_i64)]),
+    "sgc_coo_to_csr_cpu": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _p, _p, _p,
+                                          ctypes.POINTER(_u32)]),
+    "sgc_spmm_csr_f32_cpu": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
+                                            _i32]),
+    "sgc_propagate_cpu_workspace": (_i64, [_i64, _i64, _i32]),
+    "sgc_propagate_f32_cpu": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _i32,
+                                             _p, _i64, _i32]),
 }
 
 ABI_VERSION = 1

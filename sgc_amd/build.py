@@ -13,8 +13,14 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsgc_amd.so")
 SOURCES = ["capi.hip", "spmm.hip", "ingest.hip", "linear.hip", "normalize.hip", "xent.hip",
-           "subgraph.hip"]
-HEADERS = [os.path.join(CSRC, "common.h"), os.path.join(ROOT, "include", "sgc_amd.h")]
+           "subgraph.hip", "cpu.hip"]
+
+
+def _headers():
+    """Every header a source may include (csrc/*.h and the public ABI)."""
+    import glob
+    return sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include",
+                                                                        "sgc_amd.h")]
 ARCH = os.environ.get("SGC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -37,7 +43,7 @@ def _stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + HEADERS
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + _headers()
     return any(os.path.getmtime(d) > t for d in deps)
 
 

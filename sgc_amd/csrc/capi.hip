@@ -55,6 +55,18 @@ int subgraph_fill(const int32_t *row_ptr, const int32_t *col, const double *val,
                   int32_t *out_col, double *out_val, void *ws, int64_t ws_bytes, hipStream_t s);
 int set_tuning(const char *key, int64_t value);
 int64_t get_tuning(const char *key);
+int timing_enable(int on);
+int timing_collect(float *light_ms, float *hub_ms, int64_t capacity, int64_t *n_host);
+int coo_to_csr_cpu(const int64_t *rows, const int64_t *cols, const float *vals, int64_t nnz,
+                   int64_t n_rows, int64_t n_cols, int32_t *row_ptr, int32_t *col_idx,
+                   float *val_out, uint32_t *status_host);
+int spmm_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val, int64_t row_begin,
+             int64_t row_end, const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
+             int32_t n_threads);
+int64_t propagate_cpu_workspace(int64_t n_rows, int64_t F, int32_t K);
+int propagate_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                  int64_t n_rows, const float *X0, int64_t ldx, float *out, int64_t ldo, int64_t F,
+                  int32_t K, void *workspace, int64_t workspace_bytes, int32_t n_threads);
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                       int64_t ldy, int64_t M, int64_t K, int64_t C, hipStream_t stream);
 
@@ -237,6 +249,40 @@ int sgc_linear_xent_f32(const float *X, int64_t ldx, const float *W, const float
                         int64_t workspace_bytes, void *stream) {
     return linear_xent_f32(X, ldx, W, b, labels, M, K, C, loss, dW, db, logits, ldl, workspace,
                            workspace_bytes, as_stream(stream));
+}
+
+int sgc_timing_enable(int on) { return timing_enable(on); }
+
+int sgc_timing_collect(float *light_ms_host, float *hub_ms_host, int64_t capacity,
+                       int64_t *n_host) {
+    return timing_collect(light_ms_host, hub_ms_host, capacity, n_host);
+}
+
+/* ---- host (CPU) twins ---------------------------------------------------- */
+
+int sgc_coo_to_csr_cpu(const int64_t *rows, const int64_t *cols, const float *vals, int64_t nnz,
+                       int64_t n_rows, int64_t n_cols, int32_t *row_ptr, int32_t *col_idx,
+                       float *val_out, uint32_t *status_host) {
+    return coo_to_csr_cpu(rows, cols, vals, nnz, n_rows, n_cols, row_ptr, col_idx, val_out,
+                          status_host);
+}
+
+int sgc_spmm_csr_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                         int64_t row_begin, int64_t row_end, const float *X, int64_t ldx,
+                         float *Y, int64_t ldy, int64_t F, int32_t n_threads) {
+    return spmm_cpu(row_ptr, col_idx, val, row_begin, row_end, X, ldx, Y, ldy, F, n_threads);
+}
+
+int64_t sgc_propagate_cpu_workspace(int64_t n_rows, int64_t F, int32_t K) {
+    return propagate_cpu_workspace(n_rows, F, K);
+}
+
+int sgc_propagate_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                          int64_t n_rows, const float *X0, int64_t ldx, float *out, int64_t ldo,
+                          int64_t F, int32_t K, void *workspace, int64_t workspace_bytes,
+                          int32_t n_threads) {
+    return propagate_cpu(row_ptr, col_idx, val, n_rows, X0, ldx, out, ldo, F, K, workspace,
+                         workspace_bytes, n_threads);
 }
 
 }  // extern "C"

@@ -540,12 +540,17 @@ struct LaunchArgs {
     hipStream_t stream;
 };
 
-// A side stream + fork/join events per device for the hub kernel (runs beside
-// the main kernel; ordered against the caller's stream by events, so the pair
-// is capturable into a hipGraph).
+// A side stream + fork/join events per (device, priority) for the hub kernel
+// (runs beside the main kernel; ordered against the caller's stream by
+// events, so the pair is capturable into a hipGraph).  The whole fork ->
+// launch -> join sequence of one sgc_spmm call runs under `mu`: another host
+// thread can neither re-record `fork` between this call's record and wait
+// (which would order the hub kernel after the wrong stream) nor enqueue on
+// the side stream while a capture holds it.
 struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    std::mutex mu;
 };
 
 // Hub-kernel stream priority: 1 = the device's highest (meant to let a
@@ -578,6 +583,29 @@ hipError_t side_stream(SideStream **out) {
     }
     *out = &ss;
     return hipSuccess;
+}
+
+// Launch timing (diagnostics, off by default; bench.py turns it on over its
+// timed region): each launch_spmm records timing events around its
+// light/heavy kernel and around its hub kernel, each on the stream the kernel
+// runs on, so the two kernels' durations are measured separately.
+// sgc_timing_collect() waits for and returns them.  Not for use inside a
+// graph capture.
+struct TimedLaunch {
+    hipEvent_t l0 = nullptr, l1 = nullptr, h0 = nullptr, h1 = nullptr;
+};
+static std::mutex g_timing_mu;
+static bool g_timing = false;
+static std::vector<TimedLaunch> g_timed;
+static std::vector<hipEvent_t> g_event_pool;
+
+hipError_t pooled_event(hipEvent_t *e) {
+    if (!g_event_pool.empty()) {
+        *e = g_event_pool.back();
+        g_event_pool.pop_back();
+        return hipSuccess;
+    }
+    return hipEventCreate(e);
 }
 
 // Nonzeros per step: light items keep U*C*V <= ~40 registers of gathered X
@@ -708,6 +736,12 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     }
     n_hub = std::max<int64_t>(0, std::min<int64_t>(n_hub, n_heavy));
     SideStream *side = nullptr;
+    std::unique_lock<std::mutex> side_lock;
+    std::unique_lock<std::mutex> timing_lock(g_timing_mu);
+    TimedLaunch tl;
+    const bool timing = g_timing;
+    if (!timing) timing_lock.unlock();
+    hipStream_t light_stream = stream;
     if (n_hub > 0) {
         // hub rows (the heaviest n_hub of the plan) run on the side stream
         // 32-feature chunks spread a hub over more CUs; measured faster up to
@@ -718,9 +752,16 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         const int n_chunks = (int)((F + hc - 1) / hc);
         SGC_REQUIRE(n_hub * n_chunks < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many hub items");
         SGC_HIP_CHECK(side_stream(&side));
+        side_lock = std::unique_lock<std::mutex>(side->mu);
         SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
         SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
         hipStream_t hs = g_hub_first ? stream : side->s;
+        light_stream = g_hub_first ? side->s : stream;
+        if (timing) {
+            SGC_HIP_CHECK(pooled_event(&tl.h0));
+            SGC_HIP_CHECK(pooled_event(&tl.h1));
+            SGC_HIP_CHECK(hipEventRecord(tl.h0, hs));
+        }
         if (hc == 32)
             hipLaunchKernelGGL(spmm_hub_kernel<32>, dim3((unsigned)(n_hub * n_chunks)), dim3(1024),
                                0, hs, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
@@ -730,6 +771,7 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
                                0, hs, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
                                (int)F, heavy_rows, n_chunks);
         SGC_HIP_CHECK(hipGetLastError());
+        if (timing) SGC_HIP_CHECK(hipEventRecord(tl.h1, hs));
         heavy_rows += n_hub;
         n_heavy -= n_hub;
     }
@@ -745,8 +787,12 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     SGC_REQUIRE(slices < 65536, SGC_ERANGE, "spmm: too many feature slices");
 
     LaunchArgs a{row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)n_rows, (int)F,
-                 heavy_rows, (int)n_heavy, heavy_threshold, slices,
-                 side && g_hub_first ? side->s : stream};
+                 heavy_rows, (int)n_heavy, heavy_threshold, slices, light_stream};
+    if (timing) {
+        SGC_HIP_CHECK(pooled_event(&tl.l0));
+        SGC_HIP_CHECK(pooled_event(&tl.l1));
+        SGC_HIP_CHECK(hipEventRecord(tl.l0, light_stream));
+    }
     hipError_t e;
     if (V == 4)
         e = dispatch_c<4, max_chunks(4)>(C, a);
@@ -755,10 +801,44 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     else
         e = dispatch_c<1, max_chunks(1)>(C, a);
     SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "spmm launch failed: %s", hipGetErrorString(e));
+    if (timing) {
+        SGC_HIP_CHECK(hipEventRecord(tl.l1, light_stream));
+        g_timed.push_back(tl);
+    }
     if (side) {  // join: the caller's stream waits for the hub kernel
         SGC_HIP_CHECK(hipEventRecord(side->join, side->s));
         SGC_HIP_CHECK(hipStreamWaitEvent(stream, side->join, 0));
     }
+    return SGC_OK;
+}
+
+int timing_enable(int on) {
+    std::lock_guard<std::mutex> lock(g_timing_mu);
+    g_timing = on != 0;
+    return SGC_OK;
+}
+
+int timing_collect(float *light_ms, float *hub_ms, int64_t capacity, int64_t *n_host) {
+    SGC_REQUIRE(n_host, SGC_EINVAL, "timing_collect: null n_host");
+    std::lock_guard<std::mutex> lock(g_timing_mu);
+    const int64_t n = (int64_t)g_timed.size();
+    *n_host = n;
+    SGC_REQUIRE(capacity >= n && (n == 0 || (light_ms && hub_ms)), SGC_ENOMEM,
+                "timing_collect: capacity %lld < %lld launches", (long long)capacity,
+                (long long)n);
+    for (int64_t i = 0; i < n; ++i) {
+        TimedLaunch &t = g_timed[(size_t)i];
+        SGC_HIP_CHECK(hipEventSynchronize(t.l1));
+        SGC_HIP_CHECK(hipEventElapsedTime(&light_ms[i], t.l0, t.l1));
+        hub_ms[i] = -1.0f;
+        if (t.h0) {
+            SGC_HIP_CHECK(hipEventSynchronize(t.h1));
+            SGC_HIP_CHECK(hipEventElapsedTime(&hub_ms[i], t.h0, t.h1));
+        }
+        for (hipEvent_t ev : {t.l0, t.l1, t.h0, t.h1})
+            if (ev) g_event_pool.push_back(ev);
+    }
+    g_timed.clear();
     return SGC_OK;
 }
 

@@ -3,12 +3,16 @@
 SGC (reference models.py:7-18) is logistic regression over the propagated
 features: an nn.Linear(nfeat, nclass) held as attribute `.W` (callers and
 optimisers see the same parameters: .W.weight [nclass, nfeat], .W.bias).
-The forward GEMM runs on the fp32 MFMA kernel (sgc_linear_f32); the backward
-(dW = dY^T X, db = sum dY, dX = dY W) is three small torch ops, so Adam
-(citation.py:41) and LBFGS (reddit.py:52) work unchanged.
+On ROCm tensors the forward GEMM runs on the fp32 MFMA kernel
+(sgc_linear_f32); the backward (dW = dY^T X, db = sum dY, dX = dY W) is three
+small torch ops, so Adam (citation.py:41) and LBFGS (reddit.py:52) work
+unchanged.  On CPU tensors (the reference's --no-cuda mode) the forward is the
+reference's own nn.Linear arithmetic, so CPU runs reproduce its results bit
+for bit.
 """
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .propagate import linear as _mfma_linear
 from .propagate import linear_xent as _fused_xent
@@ -54,7 +58,10 @@ def sgc_cross_entropy(model, features, labels):
     """F.cross_entropy(model(features), labels) for an SGC model, fused on the
     GPU: one launch chain computes the loss and the W/b gradients (the
     reference closure, citation.py:47-49 / reddit.py:55-58).  Works with Adam
-    and LBFGS exactly like the unfused expression."""
+    and LBFGS exactly like the unfused expression.  CPU tensors take the
+    unfused expression itself."""
+    if features.device.type == "cpu":
+        return F.cross_entropy(model(features), labels)
     return _LinearCrossEntropy.apply(features, model.W.weight, model.W.bias, labels)
 
 
@@ -66,6 +73,8 @@ class SGC(nn.Module):
         self.W = nn.Linear(nfeat, nclass)
 
     def forward(self, x):
+        if x.device.type == "cpu":  # reference arithmetic (models.py:18)
+            return self.W(x)
         return _LinearMFMA.apply(x, self.W.weight, self.W.bias)
 
 

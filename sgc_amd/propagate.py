@@ -2,7 +2,10 @@
 
 This is the engine under the drop-in `sgc_precompute` (reference
 utils.py:92-97).  Host code only marshals torch tensors into the C ABI
-(include/sgc_amd.h); every byte of arithmetic runs in the HIP kernels.
+(include/sgc_amd.h); every byte of arithmetic runs in the HIP kernels for
+ROCm tensors, and in the library's host twins (sgc_*_cpu, C++ threads) for
+CPU tensors -- the reference's own CPU mode (args.py:39 --no-cuda).  A ROCm
+tensor never takes the CPU path: mixed devices raise, as torch.spmm does.
 """
 import os
 from dataclasses import dataclass, field
@@ -66,9 +69,15 @@ def _require_device(t, what):
             "ROCm (gfx950) device -- move tensors with .cuda() (no CPU fallback)")
 
 
+def cpu_threads():
+    """Threads of the host path: torch's intra-op setting (torch.set_num_threads)."""
+    return max(1, torch.get_num_threads())
+
+
 @dataclass
 class DeviceCSR:
-    """int32 CSR of the normalised adjacency S, resident in HBM.
+    """int32 CSR of the normalised adjacency S, resident in HBM (or in host
+    memory for a CPU adjacency).
 
     Built once per adjacency tensor (cached on it) by a stable sort of the
     COO entries by row: every stored entry is kept and each row keeps its
@@ -104,6 +113,8 @@ class DeviceCSR:
     def from_torch(cls, adj):
         """From a torch sparse COO (reference utils.py:23-30 layout) or CSR tensor."""
         import time
+        if isinstance(adj, torch.Tensor) and adj.device.type == "cpu":
+            return cls._from_torch_cpu(adj)
         _require_device(adj, "adj")
         if adj.dtype != torch.float32:
             raise TypeError(f"sgc_amd: adj must be float32, got {adj.dtype}")
@@ -147,6 +158,40 @@ class DeviceCSR:
                                                 ctypes_byref(status), stream), "csr64_to_csr")
             else:
                 raise TypeError(f"sgc_amd: unsupported adj layout {adj.layout}")
+        csr = cls(n_rows, n_cols, row_ptr, col_idx, val, int(status.value))
+        csr.ingest_seconds = time.perf_counter() - t0
+        return csr
+
+    @classmethod
+    def _from_torch_cpu(cls, adj):
+        """Host CSR of a CPU adjacency (sgc_coo_to_csr_cpu: stable by row)."""
+        import time
+        if adj.dtype != torch.float32:
+            raise TypeError(f"sgc_amd: adj must be float32, got {adj.dtype}")
+        if adj.dim() != 2:
+            raise ValueError("sgc_amd: adj must be 2-D")
+        lib = _lib.load()
+        n_rows, n_cols = adj.shape
+        t0 = time.perf_counter()
+        if adj.layout == torch.sparse_coo:
+            idx = adj._indices().contiguous()
+            vals = adj._values().contiguous()
+        elif adj.layout == torch.sparse_csr:
+            crow = adj.crow_indices().to(torch.int64)
+            rows = torch.repeat_interleave(torch.arange(n_rows, dtype=torch.int64),
+                                           crow[1:] - crow[:-1])
+            idx = torch.stack([rows, adj.col_indices().to(torch.int64)])
+            vals = adj.values().contiguous()
+        else:
+            raise TypeError(f"sgc_amd: unsupported adj layout {adj.layout}")
+        nnz = vals.numel()
+        row_ptr = torch.empty(n_rows + 1, dtype=torch.int32)
+        col_idx = torch.empty(nnz, dtype=torch.int32)
+        val = torch.empty(nnz, dtype=torch.float32)
+        status = _lib._u32(0)
+        _lib.check(lib.sgc_coo_to_csr_cpu(_lib.ptr(idx[0]), _lib.ptr(idx[1]), _lib.ptr(vals), nnz,
+                                          n_rows, n_cols, _lib.ptr(row_ptr), _lib.ptr(col_idx),
+                                          _lib.ptr(val), ctypes_byref(status)), "coo_to_csr_cpu")
         csr = cls(n_rows, n_cols, row_ptr, col_idx, val, int(status.value))
         csr.ingest_seconds = time.perf_counter() - t0
         return csr
@@ -232,7 +277,10 @@ def csr_of(adj):
 
 
 def _check_features(X, csr):
-    _require_device(X, "features")
+    if not isinstance(X, torch.Tensor):
+        raise TypeError("sgc_amd: features must be a torch.Tensor")
+    if csr.device.type != "cpu":
+        _require_device(X, "features")
     if X.device != csr.device:
         raise RuntimeError(f"sgc_amd: features on {X.device} but adj on {csr.device}")
     if X.dtype != torch.float32:
@@ -255,8 +303,14 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
         out = torch.empty((row_end - row_begin, F), dtype=torch.float32, device=X.device)
     if F == 0 or row_end == row_begin:
         return out
-    pl = csr.plan(row_begin, row_end, threshold, hub_threshold, F) if use_plan else NO_PLAN
     lib = _lib.load()
+    if X.device.type == "cpu":
+        _lib.check(lib.sgc_spmm_csr_f32_cpu(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
+                                            _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
+                                            X.stride(0), _lib.ptr(out), out.stride(0), F,
+                                            cpu_threads()), "spmm_csr_f32_cpu")
+        return out
+    pl = csr.plan(row_begin, row_end, threshold, hub_threshold, F) if use_plan else NO_PLAN
     with torch.cuda.device(X.device):
         _lib.check(lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
                                         _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
@@ -307,8 +361,16 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
         if K <= 0:
             out.copy_(X)
         return out
-    pl = csr.plan(0, n, threshold, hub_threshold, F) if use_plan else NO_PLAN
     lib = _lib.load()
+    if X.device.type == "cpu":  # host twin (reference CPU mode), same bits
+        ws_bytes = lib.sgc_propagate_cpu_workspace(n, F, int(K))
+        ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8)
+        _lib.check(lib.sgc_propagate_f32_cpu(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
+                                             _lib.ptr(csr.val), n, _lib.ptr(X), X.stride(0),
+                                             _lib.ptr(out), out.stride(0), F, int(K), _lib.ptr(ws),
+                                             ws_bytes, cpu_threads()), "propagate_f32_cpu")
+        return out
+    pl = csr.plan(0, n, threshold, hub_threshold, F) if use_plan else NO_PLAN
     stream = _lib.stream_handle(X.device)
     ldw = aligned_ld(F)
     with torch.cuda.device(X.device):
@@ -321,10 +383,14 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                                              _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
                                              _lib.ptr(ws), ws_bytes, stream), "propagate_f32")
             return out
+        pad = _needs_pad(X) and pad_pays(csr, F)
+        # buffers actually used: the re-laid X_0 (if any) + up to two
+        # ping-pong intermediates (the last hop writes `out`)
+        n_bufs = min(2, int(pad) + min(K - 1, 2))
         bufs = [torch.empty((n, ldw), dtype=torch.float32, device=X.device)
-                for _ in range(2 if K >= 2 else 1)]
+                for _ in range(n_bufs)]
         src, nxt = X, 0
-        if _needs_pad(X) and pad_pays(csr, F):
+        if pad:
             _lib.check(lib.sgc_pad_rows_f32(_lib.ptr(X), X.stride(0), _lib.ptr(bufs[0]), ldw, n, F,
                                             stream), "pad_rows_f32")
             src, nxt = bufs[0][:, :F], 1 % len(bufs)
@@ -389,6 +455,27 @@ class GraphedPropagation:
         return self.out
 
 
+def kernel_timing(on: bool):
+    """Turn per-kernel launch timing on/off (sgc_timing_enable; diagnostics)."""
+    _lib.check(_lib.load().sgc_timing_enable(1 if on else 0), "timing_enable")
+
+
+def collect_kernel_timing(capacity=1 << 16):
+    """(light_ms, hub_ms) lists of the SpMM launches recorded since the last
+    collect; hub_ms[i] is None for a launch without hub rows (synchronous)."""
+    import ctypes
+    lib = _lib.load()
+    light = (ctypes.c_float * capacity)()
+    hub = (ctypes.c_float * capacity)()
+    n = _lib._i64(0)
+    _lib.check(lib.sgc_timing_collect(ctypes.cast(light, ctypes.c_void_p),
+                                      ctypes.cast(hub, ctypes.c_void_p), capacity,
+                                      ctypes_byref(n)), "timing_collect")
+    k = int(n.value)
+    return [float(light[i]) for i in range(k)], [float(hub[i]) if hub[i] >= 0 else None
+                                                 for i in range(k)]
+
+
 def linear(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, out=None):
     """Y = X . W^T + b on fp32 MFMA (reference models.py:17-18, nn.Linear)."""
     _require_device(X, "input")
@@ -432,6 +519,14 @@ def linear_xent(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tens
     W = weight.detach().contiguous()
     b = bias.detach().contiguous() if bias is not None else None
     y = labels.to(device=X.device, dtype=torch.int64).contiguous()
+    if M:
+        # F.cross_entropy raises on a label outside [0, C) (and skips
+        # ignore_index=-100 rows, which the fused kernel does not support):
+        # refuse loudly instead of returning a silently different loss
+        lo, hi = (int(v) for v in torch.aminmax(y))
+        if lo < 0 or hi >= C:
+            raise ValueError(f"sgc_amd.linear_xent: labels must lie in [0, {C}), got "
+                             f"[{lo}, {hi}] (ignore_index is not supported)")
     lib = _lib.load()
     loss = torch.empty((), dtype=torch.float32, device=X.device)
     dW = torch.empty_like(W)

@@ -74,11 +74,13 @@ def _reddit_adjs(adj, train_index, normalization, cuda):
 
 
 def sgc_precompute(features, adj, degree):
-    """X_K = S^K X on the GPU; returns (features_K, seconds) like utils.py:92-97.
+    """X_K = S^K X; returns (features_K, seconds) like utils.py:92-97.
 
+    ROCm tensors run on the HIP kernels, CPU tensors on the library's host
+    twin (the reference's --no-cuda mode); mixed devices raise RuntimeError.
     degree <= 0 returns the input tensor object itself (the reference's loop
     body never runs).  The result is bit-identical to the reference's
-    torch.spmm chain on CPU for the same inputs."""
+    torch.spmm chain on CPU for the same inputs, on either device."""
     if degree <= 0:
         t = perf_counter()
         return features, perf_counter() - t
@@ -88,7 +90,8 @@ def sgc_precompute(features, adj, degree):
     t = perf_counter()
     csr = csr_of(adj)
     out = propagate(csr, features, degree)
-    torch.cuda.synchronize(dev)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
     return out, perf_counter() - t
 
 

@@ -155,11 +155,14 @@ def shape_case(shape, Ks, seed=0, fseed=1):
     rec = {"n": n, "edges": E, "features": F, "seed": seed, "feature_seed": fseed,
            "nnz": int(vals.shape[0]), "sha_indices": sha(idx), "sha_values": sha(vals),
            "sha_X": sha(X), "generate_seconds": round(gen_s, 2), "outputs": {}}
+    del A, u, v, idx, vals
     rows_pick = np.random.default_rng(99).choice(n, 16, replace=False)
     samples = {f"{shape}_rows": rows_pick}
     adj_t = adj
     for K in Ks:
-        ref_prop(X, adj_t, 1)  # warm-up (allocator first touch)
+        # warm-up (allocator first touch); at RMAT scale (260 M nnz, ~31 s per
+        # single-threaded COO hop) only on 8 feature columns
+        ref_prop(np.ascontiguousarray(X[:, :8]) if n > 10**6 else X, adj_t, 1)
         t0 = time.perf_counter()
         Y = ref_prop(X, adj_t, K)
         dt = time.perf_counter() - t0
@@ -171,16 +174,20 @@ def shape_case(shape, Ks, seed=0, fseed=1):
 
 
 def main():
-    cases = tiny_cases()
-    flat = {}
-    for name, d in cases.items():
-        for k, v in d.items():
-            flat[f"{name}/{k}"] = v
-    np.savez_compressed(os.path.join(HERE, "tiny_cases.npz"), **flat)
-    print(f"tiny cases: {len(cases)}")
-
-    which = sys.argv[1:] or ["cora", "pubmed", "reddit"]
-    Ks = {"cora": (1, 2, 3), "pubmed": (1, 2), "reddit": (2,)}
+    """python gen_golden.py [tiny] [cora] [pubmed] [reddit] [rmat]; no argument =
+    tiny + cora + pubmed + reddit.  rmat (4.19 M nodes, 260 M nnz, F=256, K=3)
+    needs ~35 GB of host memory and ~5 minutes."""
+    which = sys.argv[1:] or ["tiny", "cora", "pubmed", "reddit"]
+    if "tiny" in which:
+        cases = tiny_cases()
+        flat = {}
+        for name, d in cases.items():
+            for k, v in d.items():
+                flat[f"{name}/{k}"] = v
+        np.savez_compressed(os.path.join(HERE, "tiny_cases.npz"), **flat)
+        print(f"tiny cases: {len(cases)}")
+    which = [w for w in which if w != "tiny"]
+    Ks = {"cora": (1, 2, 3), "pubmed": (1, 2), "reddit": (2,), "rmat": (3,)}
     out_json = os.path.join(HERE, "shapes.json")
     meta = json.load(open(out_json)) if os.path.exists(out_json) else {}
     rows_path = os.path.join(HERE, "shape_rows.npz")

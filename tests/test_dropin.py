@@ -207,18 +207,19 @@ def test_model_surface():
         get_model("GCN", 20, 3, cuda=False)
 
 
-def test_cpu_tensors_fail_loudly():
-    """No CPU fallback anywhere on the product path."""
+def test_cpu_tensors_run_like_the_reference():
+    """CPU tensors take the library's host twin (reference --no-cuda mode,
+    args.py:39), not an error; K=0 returns the input object."""
     from sgc_amd.models import SGC
     from sgc_amd.utils import sgc_precompute
     adj = torch.sparse_coo_tensor(torch.tensor([[0, 1], [1, 0]]), torch.tensor([1.0, 1.0]), (2, 2))
-    X = torch.ones(2, 3)
-    with pytest.raises(RuntimeError, match="ROCm"):
-        sgc_precompute(X, adj, 2)
+    X = torch.arange(6, dtype=torch.float32).reshape(2, 3)
+    out, _ = sgc_precompute(X, adj, 1)
+    assert torch.equal(out, torch.spmm(adj, X))
     out, _ = sgc_precompute(X, adj, 0)  # K=0: the input object, as the reference
     assert out is X
-    with pytest.raises(RuntimeError, match="ROCm"):
-        SGC(3, 2)(X)
+    m = SGC(3, 2)
+    assert torch.equal(m(X), m.W(X))
 
 
 def test_dropin_modules_reexport():

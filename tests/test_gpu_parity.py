@@ -217,6 +217,103 @@ def test_reddit_shape_hash(shapes_golden, shape_rows):
     assert sha(Y) == g["outputs"]["2"]["sha"]
 
 
+@pytest.mark.slow
+def test_rmat_shape_hash(shapes_golden, shape_rows):
+    """BASELINE config 5 at full size (4,194,304 nodes, 260,194,304 nnz, F=256,
+    K=3): bit-exact hash of the whole X_3 against the reference's own
+    sgc_precompute (tests/golden/gen_golden.py rmat, run in the build
+    container: reference aug_normalized_adjacency + sparse_mx_to_torch_sparse_
+    tensor + torch.spmm COO, 308 s on one CPU thread)."""
+    if "rmat" not in shapes_golden:
+        pytest.skip("rmat golden not generated")
+    from sgc_amd import graphs
+    from sgc_amd.propagate import DeviceCSR, propagate
+    g = shapes_golden["rmat"]
+    S = graphs.synthetic_graph("rmat", seed=g["seed"])
+    rows, cols, vals = S.coo()
+    assert sha(np.stack([rows, cols])) == g["sha_indices"]
+    assert sha(vals) == g["sha_values"]
+    del rows, cols, vals
+    X = graphs.synthetic_features("rmat", g["n"], g["features"], seed=g["feature_seed"])
+    assert sha(X) == g["sha_X"]
+    csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val)
+    Xd = torch.from_numpy(X)
+    del X
+    Y = propagate(csr, Xd.to(DEV), 3).cpu().numpy()
+    assert bits_equal(Y[shape_rows["rmat_rows"]], shape_rows["rmat_K3"])
+    assert sha(Y) == g["outputs"]["3"]["sha"]
+
+
+@pytest.mark.parametrize("F", [64, 130, 192])
+@pytest.mark.parametrize("hub_chunk", [32, 64])
+def test_long_hub_rows_bit_exact(oracle, F, hub_chunk):
+    """Hub rows of 7,000 / 3,001 / 2,881 nonzeros on the LDS-staged hub kernel:
+    several kHubUnroll iterations (2,880 nonzeros each at HC=32), the
+    register-ring and column-id parity wrap, and ragged last rounds, on
+    128-B aligned rows (HC=32 is what the row partition's narrow feature
+    groups use).  Oracle: the CPU restatement of torch.spmm's arithmetic."""
+    from sgc_amd import _lib, graphs
+    from sgc_amd.propagate import DeviceCSR, propagate
+    rng = np.random.default_rng(F + hub_chunk)
+    n = 9000
+    u = [np.zeros(7000, np.int64), np.full(3001, 1, np.int64), np.full(2881, 2, np.int64)]
+    v = [np.arange(1000, 8000), np.arange(3000, 6001), np.arange(5000, 7881)]
+    ru, rv = rng.integers(3, n, 20000), rng.integers(3, n, 20000)
+    keep = ru != rv
+    lo = np.concatenate(u + [np.minimum(ru, rv)[keep]])
+    hi = np.concatenate(v + [np.maximum(ru, rv)[keep]])
+    key = np.unique(lo * n + hi)
+    S = graphs.aug_norm_csr_from_pairs(n, key // n, key % n)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    want = oracle.propagate(S.row_ptr, S.col_idx, S.val, X, 2)
+    lib = _lib.load()
+    _lib.check(lib.sgc_set_tuning(b"hub_chunk", hub_chunk), "set_tuning")
+    try:
+        csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val)
+        pl = csr.plan(0, n, 64, 1000, F)
+        assert pl.n_hub == 3
+        Xd = torch.zeros((n, (F + 31) // 32 * 32), device=DEV)[:, :F]  # 128-B rows
+        Xd.copy_(torch.from_numpy(X))
+        out = propagate(csr, Xd, 2, threshold=64, hub_threshold=1000)
+        torch.cuda.synchronize()
+        assert bits_equal(out.cpu().numpy(), want)
+    finally:
+        lib.sgc_set_tuning(b"hub_chunk", 0)
+
+
+def test_fused_xent_rejects_bad_labels():
+    from sgc_amd.propagate import linear_xent
+    X = torch.randn(10, 8, device=DEV)
+    W = torch.randn(3, 8, device=DEV)
+    b = torch.zeros(3, device=DEV)
+    for bad in (3, -1, -100):
+        y = torch.zeros(10, dtype=torch.int64, device=DEV)
+        y[4] = bad
+        with pytest.raises(ValueError):
+            linear_xent(X, W, b, y)
+
+
+def test_kernel_timing_hooks(tiny_cases):
+    """sgc_timing_*: one (light, hub) pair per SpMM launch, hub None without hubs."""
+    from sgc_amd.propagate import (DeviceCSR, collect_kernel_timing, kernel_timing,
+                                   propagate)
+    c = tiny_cases["hub1000_F130"]
+    csr = DeviceCSR.from_torch(coo_cuda(c))
+    X = torch.from_numpy(c["X"]).to(DEV)
+    collect_kernel_timing()
+    kernel_timing(True)
+    try:
+        out = propagate(csr, X, 2, threshold=3, hub_threshold=5)
+        propagate(csr, X, 1, threshold=10**9, hub_threshold=10**9)
+    finally:
+        kernel_timing(False)
+    light, hub = collect_kernel_timing()
+    assert len(light) == 3 and all(t > 0 for t in light)
+    assert hub[0] > 0 and hub[1] > 0 and hub[2] is None
+    assert bits_equal(out.cpu().numpy(), c["Y2"])
+    assert collect_kernel_timing() == ([], [])
+
+
 @pytest.mark.parametrize("M,K,C", [(1, 3, 1), (140, 1433, 7), (333, 602, 41), (1000, 500, 3),
                                    (77, 64, 64), (50, 130, 100), (2048, 602, 41)])
 def test_linear_mfma_vs_torch_fp32(M, K, C):
