@@ -441,7 +441,14 @@ def main():
                     help="N>1 features, replicated output: row chunks of the last hop")
     ap.add_argument("--alt-steps", type=int, default=5,
                     help="N>1: steps timed with the other output mode (0 = skip)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="schedule knob for sgc_set_tuning (results never depend on it)")
     args = ap.parse_args()
+    if args.tune:
+        from sgc_amd import _lib
+        for kv in args.tune:
+            k, v = kv.split("=", 1)
+            _lib.check(_lib.load().sgc_set_tuning(k.encode(), int(v)), f"set_tuning {kv}")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -471,6 +478,8 @@ def main():
            "warmup": args.warmup, "higher_is_better": True, "scaling": "strong",
            "vs_baseline": None, "dtype": "f32",
            "data": "synthetic (seeded R-MAT graph + AugNorm, SURVEY.md 8(d))"}
+    if args.tune:
+        rec["tuning"] = args.tune
 
     if not distributed:
         main_rec, S, X_host = single_gpu_shape(args.shape, args, dev, lib_sha, args.steps,

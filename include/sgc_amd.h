@@ -54,7 +54,10 @@ const char *sgc_last_error(void);
  *                   32 when F <= 192 and X rows are 128-B aligned, else 64);
  *   "hub_priority": 1 = hub kernel on a highest-priority stream (default 0);
  *   "hub_first":    1 = hub kernel on the caller's stream, the light/heavy
- *                   kernel on the side stream (default 0: the reverse).
+ *                   kernel on the side stream (default 0: the reverse);
+ *   "rows_per_wave": light rows per wavefront when 16-B lanes are possible
+ *                   (2 = default: 32 lanes x 4 floats per row; 4; 1 = one row
+ *                   per wave with the slice_floats / max_vec scheme).
  * sgc_get_tuning returns -1 for an unknown key. */
 int sgc_set_tuning(const char *key, int64_t value);
 int64_t sgc_get_tuning(const char *key);
@@ -189,6 +192,26 @@ int sgc_spmm_csr_f32(const int32_t *row_ptr, const int32_t *col_idx, const float
 int sgc_timing_enable(int on);
 int sgc_timing_collect(float *light_ms_host, float *hub_ms_host, int64_t capacity,
                        int64_t *n_host);
+
+/* Same, with flags.
+ * Layout, for buffers whose rows are padded (the engine's own 128-B-row
+ * buffers): SGC_SPMM_X_PADDED = X's columns [F, round4(F)) are allocated in
+ * every row and may be read (their values do not matter); SGC_SPMM_Y_PADDED
+ * = Y's columns [F, round4(F)) are allocated and may be overwritten with
+ * don't-care values.  They let the kernel use 16-B lanes at any F; columns
+ * < F are bit-identical either way.
+ * Split launch of one hop (the multi-GPU pipeline runs the hub rows beside
+ * several narrower launches): SGC_SPMM_NO_HUB = skip the plan's n_hub hub
+ * rows (their Y rows are not written); SGC_SPMM_HUB_ONLY = only the hub rows,
+ * on `stream` itself (no side stream).  The two launches together write
+ * exactly what one unflagged launch writes. */
+enum { SGC_SPMM_X_PADDED = 1, SGC_SPMM_Y_PADDED = 2, SGC_SPMM_NO_HUB = 4,
+       SGC_SPMM_HUB_ONLY = 8 };
+int sgc_spmm_csr_f32_ex(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                        int64_t row_begin, int64_t row_end,
+                        const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
+                        const int32_t *plan, int64_t n_heavy, int64_t n_hub,
+                        int32_t heavy_threshold, uint32_t flags, void *stream);
 
 /* K hops X_K = S^K X_0 over all n_rows rows (utils.py:92-97, the whole
  * sgc_precompute loop).  out (row stride ldo) receives X_K.  Intermediate

@@ -43,6 +43,8 @@ SIGNATURES = {
                                       ctypes.POINTER(_i64), _p]),
     "sgc_spmm_csr_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
                                         _p, _i64, _i64, _i32, _p]),
+    "sgc_spmm_csr_f32_ex": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
+                                           _p, _i64, _i64, _i32, _u32, _p]),
     "sgc_propagate_workspace": (_i64, [_i64, _i64, _i64, _i32]),
     "sgc_propagate_f32": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _i32,
                                          _p, _i64, _i64, _i32, _p, _i64, _p]),

@@ -29,7 +29,7 @@ int build_plan(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int32
 int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                 int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
                 int64_t ldy, int64_t F, const int32_t *heavy_rows, int64_t n_heavy,
-                int64_t n_hub, int32_t heavy_threshold, hipStream_t stream);
+                int64_t n_hub, int32_t heavy_threshold, uint32_t flags, hipStream_t stream);
 int launch_pad_rows(const float *src, int64_t lds, float *dst, int64_t ldd, int64_t n_rows,
                     int64_t F, hipStream_t stream);
 size_t augnorm_scan_temp_bytes(int64_t n);
@@ -168,7 +168,22 @@ int sgc_spmm_csr_f32(const int32_t *row_ptr, const int32_t *col_idx, const float
                      int64_t ldy, int64_t F, const int32_t *plan, int64_t n_heavy,
                      int64_t n_hub, int32_t heavy_threshold, void *stream) {
     return launch_spmm(row_ptr, col_idx, val, row_begin, row_end, X, ldx, Y, ldy, F, plan,
-                       plan ? n_heavy : 0, plan ? n_hub : 0, heavy_threshold, as_stream(stream));
+                       plan ? n_heavy : 0, plan ? n_hub : 0, heavy_threshold, 0u,
+                       as_stream(stream));
+}
+
+int sgc_spmm_csr_f32_ex(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                        int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
+                        int64_t ldy, int64_t F, const int32_t *plan, int64_t n_heavy,
+                        int64_t n_hub, int32_t heavy_threshold, uint32_t flags, void *stream) {
+    constexpr uint32_t known = SGC_SPMM_X_PADDED | SGC_SPMM_Y_PADDED | SGC_SPMM_NO_HUB |
+                               SGC_SPMM_HUB_ONLY;
+    SGC_REQUIRE((flags & ~known) == 0, SGC_EINVAL, "spmm_ex: unknown flags 0x%x", flags);
+    SGC_REQUIRE(!((flags & SGC_SPMM_NO_HUB) && (flags & SGC_SPMM_HUB_ONLY)), SGC_EINVAL,
+                "spmm_ex: NO_HUB and HUB_ONLY together");
+    return launch_spmm(row_ptr, col_idx, val, row_begin, row_end, X, ldx, Y, ldy, F, plan,
+                       plan ? n_heavy : 0, plan ? n_hub : 0, heavy_threshold, flags,
+                       as_stream(stream));
 }
 
 int64_t sgc_aligned_ld(int64_t F) { return F <= 0 ? 0 : (F + 31) / 32 * 32; }
@@ -224,8 +239,10 @@ int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const floa
         const bool last = h == K - 1;
         float *dst = last ? out : bufs[next];
         const int64_t ldd = last ? ldo : ldw;
+        // the workspace buffers' pad columns [F, ldw) may be read and written
+        const uint32_t fl = (src != X0 ? SGC_SPMM_X_PADDED : 0u) | (last ? 0u : SGC_SPMM_Y_PADDED);
         const int rc = launch_spmm(row_ptr, col_idx, val, 0, n_rows, src, lds, dst, ldd, F, plan,
-                                   plan ? n_heavy : 0, plan ? n_hub : 0, heavy_threshold, s);
+                                   plan ? n_heavy : 0, plan ? n_hub : 0, heavy_threshold, fl, s);
         if (rc) return rc;
         src = dst;
         lds = ldd;

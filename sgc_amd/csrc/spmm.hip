@@ -43,6 +43,8 @@
 
 namespace sgc {
 
+constexpr int kBlock = 256;  // threads per light/heavy workgroup
+
 // Accumulate the C chunks [chunk0, chunk0 + C) of one row and store them.
 template <int V, int C, int U>
 __device__ __forceinline__ void row_chunks(const int *__restrict__ col,
@@ -298,6 +300,162 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Multi-row light kernel: LR lanes per row (8..32, a launch parameter), 4
+// floats per lane (one global_load_dwordx4), R = 64 / LR rows per wavefront.
+// A feature slice is LR * 4 floats: 128 at LR = 32 (2 rows per wave); a
+// narrow launch -- a 76-float feature block, a 64-float group -- takes
+// LR = width / 4 and a single slice, so up to 64 / LR rows share the wave
+// instead of leaving most lanes idle.  (spmm_csr_kernel covers a 128-float
+// slice with one row per wave and 8-B lanes: twice the load instructions for
+// the same bytes, and at most one row per wave at any width.)
+// It computes the columns up to F_load = F rounded up to 4: the engine's own
+// 128-B-row buffers hold pad columns (don't-care values, computed like any
+// other column, never returned); stores into a caller's buffer stop at F.
+//  * each row's next LB (col, val) pairs are staged in a per-wave LDS block
+//    (double buffered, loaded one block ahead); a lane reads U = 4 of its
+//    row's ids and values with one ds_read_b128 each, a broadcast within the
+//    row's LR lanes;
+//  * U nonzeros per row per step, two steps in flight (software pipelined);
+//  * the rows of one wave have different lengths: the wave runs to the
+//    longest; lanes past their row's end re-load their row's last nonzero
+//    (same lines, never out of bounds) and skip the FMAs -- still one
+//    sequential FMA chain per element in CSR order.
+// Heavy items (rows above heavy_threshold, one wave per 64*VH-float
+// sub-chunk, n_sub per slice) come first in the grid, as in spmm_csr_kernel.
+constexpr int kRowsU = 4;
+
+template <int LB, int VH, int UH>
+__global__ __launch_bounds__(256) void spmm_rows_kernel(
+    const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
+    const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
+    int row_begin, int n_rows, int F, int F_load, int LR, int vec_store, int n_sub,
+    const int *__restrict__ heavy_rows, int n_heavy, int heavy_threshold) {
+    constexpr int V = 4, U = kRowsU;
+    constexpr int kSteps = LB / U;  // steps per LDS block
+    static_assert(kSteps >= 2 && kSteps % 2 == 0, "bad block");
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) int s_col[kBlock / kWave][2][kWave];
+    __shared__ __attribute__((aligned(16))) float s_val[kBlock / kWave][2][kWave];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wl = threadIdx.x / kWave;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kBlock / kWave) + wl));
+    const int slice = blockIdx.y;
+    const int n_heavy_items = n_heavy * n_sub;
+    if (wave < n_heavy_items) {
+        const int h = wave / n_sub;
+        const int sub = slice * n_sub + (wave - h * n_sub);  // in units of 64*VH floats
+        if (sub * kWave * VH >= F) return;
+        const int row = heavy_rows[h];
+        const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
+        row_chunks_pipe<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
+                                        Y + (int64_t)(row - row_begin) * ldy, F, sub, lane);
+        return;
+    }
+    const int R = kWave / LR;  // rows per wave (uniform)
+    const int w = wave - n_heavy_items;
+    if (w * R >= n_rows) return;  // wave-uniform
+    const int sub = lane / LR, l = lane - sub * LR;
+    const int r = w * R + sub;
+    int k0 = 0, len = 0;
+    bool mine = false;
+    if (sub < R && r < n_rows) {
+        k0 = row_ptr[row_begin + r];
+        const int d = row_ptr[row_begin + r + 1] - k0;
+        mine = d <= heavy_threshold;  // longer rows: heavy items / hub kernel
+        len = mine ? d : 0;
+    }
+    int n_max = 0;
+    for (int s = 0; s < R; ++s) n_max = max(n_max, __builtin_amdgcn_readlane(len, s * LR));
+    const int f = slice * (LR * V) + l * V;
+    const bool ok = sub < R && f < F_load;
+    const uint32_t boff = ok ? uint32_t(f) * 4u : 0u;
+    const int lds_row = (sub < R ? sub : 0) * LB;  // this lane's row block in LDS
+    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (n_max > 0) {
+        const char *Xb = reinterpret_cast<const char *>(X);
+        const int64_t row_bytes = ldx * 4;
+        // lanes l < LB stage (col, val) of their row's nonzero base + l,
+        // clamped to its last one; a row without nonzeros reads X row 0 (its
+        // FMAs are all skipped)
+        const bool stager = sub < R && l < LB;
+        auto fetch = [&](int base, int &c, float &v) {
+            c = 0;
+            v = 0.0f;
+            if (len > 0 && l < LB) {
+                const int kk = k0 + min(base + l, len - 1);
+                c = col[kk];
+                v = val[kk];
+            }
+        };
+        auto stage = [&](int buf, int c, float v) {
+            if (stager) {
+                s_col[wl][buf][lds_row + l] = c;
+                s_val[wl][buf][lds_row + l] = v;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+        int colB;
+        float valB;
+        {
+            int c0;
+            float v0;
+            fetch(0, c0, v0);
+            stage(0, c0, v0);
+        }
+        fetch(LB, colB, valB);
+        f4 xv[2][U];
+        float vv[2][U];
+        auto issue = [&](int buf, int i, int slot) {
+            const i4 cc = *reinterpret_cast<const i4 *>(&s_col[wl][buf][lds_row + i * U]);
+            const f4 vq = *reinterpret_cast<const f4 *>(&s_val[wl][buf][lds_row + i * U]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                vv[slot][u] = vq[u];
+                xv[slot][u] = *reinterpret_cast<const f4 *>(Xb + (int64_t)cc[u] * row_bytes + boff);
+            }
+        };
+        issue(0, 0, 0);
+        for (int base = 0;; base += LB) {
+            const int buf = (base / LB) & 1;
+#pragma unroll
+            for (int i = 0; i < kSteps; ++i) {
+                const int cur = base + i * U;
+                if (cur >= n_max) break;  // wave-uniform
+                if (i + 1 < kSteps) {
+                    issue(buf, i + 1, (i + 1) & 1);
+                } else {  // first step of the next block, from its prefetched (col, val)
+                    stage(buf ^ 1, colB, valB);
+                    issue(buf ^ 1, 0, 0);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (cur + u < len) {
+#pragma unroll
+                        for (int v = 0; v < V; ++v)
+                            acc[v] = __builtin_fmaf(vv[i & 1][u], xv[i & 1][u][v], acc[v]);
+                    }
+                }
+            }
+            if (base + LB >= n_max) break;
+            fetch(base + 2 * LB, colB, valB);
+        }
+    }
+    if (mine && ok) {
+        float *yr = Y + (int64_t)r * ldy;
+        if (vec_store) {
+            *reinterpret_cast<f4 *>(yr + f) = acc;
+        } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if (f + v < F) yr[f + v] = acc[v];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Hub rows (degree > hub_threshold): one 1024-thread workgroup per (row,
 // HC-feature chunk).  A single wave's FMA chain over d nonzeros costs d FMAs
 // -- cheap -- but a wave keeps only ~16 nonzeros' X segments in flight, so a
@@ -324,8 +482,11 @@ constexpr int kHubLoaders = 15;
 constexpr int kHubInstr = 16;  // consecutive nonzeros per loader lane per round
 constexpr int kHubDepth = 3;   // rounds held in loader registers (17 loads each: vmcnt <= 63)
 constexpr int kHubUnroll = 6;  // lcm(kHubDepth, 2): X ring slot and colv parity compile-time
+#ifndef SGC_HUB_ASM
+#define SGC_HUB_ASM 1  // the chain loop as counted-wait asm (hub_chain_asm)
+#endif
 #ifndef SGC_HUB_PRE
-#define SGC_HUB_PRE 3
+#define SGC_HUB_PRE (SGC_HUB_ASM ? 4 : 3)
 #endif
 constexpr int kHubPre = SGC_HUB_PRE;  // LDS batches of 4 nonzeros the chain reads ahead
 #ifndef SGC_HUB_SCHED
@@ -344,6 +505,121 @@ struct HubShape {
     // for the FMA loop's read-ahead (kHubPre batches of 4 past the last full batch)
     static constexpr int kStride = (kRound + kPad + 63) / 64 * 64 + 4;
 };
+
+#ifndef SGC_HUB_STAMPS
+#define SGC_HUB_STAMPS 0  // diagnostic build only: per-round clock stamps of block 0
+#endif
+#if SGC_HUB_STAMPS
+// [0] chain wave leaves the round's barrier, [1] chain wave reaches the next
+// barrier (FMAs done), [2] loader wave 1 after its LDS store, [3] loader wave
+// 1 reaches the barrier (loads issued); [4][0..1] s_memtime / s_memrealtime
+// at kernel start and end (clock rate).  Lane 0's vector stores only; read
+// back with sgc_debug_hub_stamps (exported by this build only).
+constexpr int kStampRounds = 4096;
+__device__ unsigned long long g_hub_stamp[5][kStampRounds];
+#define HUB_STAMP(slot, r)                                                            \
+    do {                                                                              \
+        if (blockIdx.x == 0 && lane == 0 && (r) < kStampRounds)                       \
+            g_hub_stamp[slot][r] = __builtin_amdgcn_s_memtime();                      \
+    } while (0)
+#else
+#define HUB_STAMP(slot, r) \
+    do {                   \
+    } while (0)
+#endif
+
+#if SGC_HUB_ASM
+// acc = fmaf(v[k], x[k], acc) for the 4*(4*iters + rem) nonzeros of one
+// round, in order: x at LDS byte address xa (this lane's feature row of the
+// transposed image), v at va (broadcast).  Ring of four slots in v[80:111]
+// (x in v80.., v in v96..), refilled four batches (64 B) ahead; reads past
+// the round stay inside the padded image (kPad >= 16 floats).  Every LDS
+// read is complete (lgkmcnt(0)) before the block ends, so the clobbered
+// registers hold nothing in flight afterwards.  Only LDS reads and VALU.
+__device__ __forceinline__ void hub_chain_asm(float &acc, uint32_t xa, uint32_t va, int iters,
+                                              int rem) {
+    asm volatile(
+        // lgkmcnt also counts scalar loads, which complete out of order:
+        // start with nothing in flight so the counted waits below are exact
+        "s_waitcnt lgkmcnt(0)\n"
+        // prologue: batches 0..3 into slots 0..3
+        "ds_read_b128 v[80:83], %[xa]\n"
+        "ds_read_b128 v[96:99], %[va]\n"
+        "ds_read_b128 v[84:87], %[xa] offset:16\n"
+        "ds_read_b128 v[100:103], %[va] offset:16\n"
+        "ds_read_b128 v[88:91], %[xa] offset:32\n"
+        "ds_read_b128 v[104:107], %[va] offset:32\n"
+        "ds_read_b128 v[92:95], %[xa] offset:48\n"
+        "ds_read_b128 v[108:111], %[va] offset:48\n"
+        "s_cmp_eq_u32 %[it], 0\n"
+        "s_cbranch_scc1 2f\n"
+        "1:\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_fmac_f32 %[acc], v96, v80\n"
+        "v_fmac_f32 %[acc], v97, v81\n"
+        "v_fmac_f32 %[acc], v98, v82\n"
+        "v_fmac_f32 %[acc], v99, v83\n"
+        "ds_read_b128 v[80:83], %[xa] offset:64\n"
+        "ds_read_b128 v[96:99], %[va] offset:64\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_fmac_f32 %[acc], v100, v84\n"
+        "v_fmac_f32 %[acc], v101, v85\n"
+        "v_fmac_f32 %[acc], v102, v86\n"
+        "v_fmac_f32 %[acc], v103, v87\n"
+        "ds_read_b128 v[84:87], %[xa] offset:80\n"
+        "ds_read_b128 v[100:103], %[va] offset:80\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_fmac_f32 %[acc], v104, v88\n"
+        "v_fmac_f32 %[acc], v105, v89\n"
+        "v_fmac_f32 %[acc], v106, v90\n"
+        "v_fmac_f32 %[acc], v107, v91\n"
+        "ds_read_b128 v[88:91], %[xa] offset:96\n"
+        "ds_read_b128 v[104:107], %[va] offset:96\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_fmac_f32 %[acc], v108, v92\n"
+        "v_fmac_f32 %[acc], v109, v93\n"
+        "v_fmac_f32 %[acc], v110, v94\n"
+        "v_fmac_f32 %[acc], v111, v95\n"
+        "ds_read_b128 v[92:95], %[xa] offset:112\n"
+        "ds_read_b128 v[108:111], %[va] offset:112\n"
+        "v_add_u32 %[xa], 64, %[xa]\n"
+        "v_add_u32 %[va], 64, %[va]\n"
+        "s_sub_u32 %[it], %[it], 1\n"
+        "s_cmp_lg_u32 %[it], 0\n"
+        "s_cbranch_scc1 1b\n"
+        "2:\n"
+        // tail: the first `rem` slots hold the last batches of the round
+        "s_cmp_gt_u32 %[rem], 0\n"
+        "s_cbranch_scc0 3f\n"
+        "s_waitcnt lgkmcnt(6)\n"
+        "v_fmac_f32 %[acc], v96, v80\n"
+        "v_fmac_f32 %[acc], v97, v81\n"
+        "v_fmac_f32 %[acc], v98, v82\n"
+        "v_fmac_f32 %[acc], v99, v83\n"
+        "s_cmp_gt_u32 %[rem], 1\n"
+        "s_cbranch_scc0 3f\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32 %[acc], v100, v84\n"
+        "v_fmac_f32 %[acc], v101, v85\n"
+        "v_fmac_f32 %[acc], v102, v86\n"
+        "v_fmac_f32 %[acc], v103, v87\n"
+        "s_cmp_gt_u32 %[rem], 2\n"
+        "s_cbranch_scc0 3f\n"
+        "s_waitcnt lgkmcnt(2)\n"
+        "v_fmac_f32 %[acc], v104, v88\n"
+        "v_fmac_f32 %[acc], v105, v89\n"
+        "v_fmac_f32 %[acc], v106, v90\n"
+        "v_fmac_f32 %[acc], v107, v91\n"
+        "3:\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [xa] "+v"(xa), [va] "+v"(va), [it] "+s"(iters)
+        : [rem] "s"(rem)
+        : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91",
+          "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102",
+          "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "scc",
+          "memory");
+}
+#endif
 
 template <int HC>
 __global__ __launch_bounds__(1024) void spmm_hub_kernel(
@@ -413,6 +689,16 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
         load_col(kHubDepth, kHubDepth & 1);
         if (n_round > 0) store(0, 0);
     }
+#if SGC_HUB_STAMPS
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        g_hub_stamp[4][0] = __builtin_amdgcn_s_memtime();
+        g_hub_stamp[4][1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+#ifndef SGC_HUB_PRIO
+#define SGC_HUB_PRIO 0  // chain-wave s_setprio level: measured neutral (+-1%), off
+#endif
+    if (SGC_HUB_PRIO && w == 0) __builtin_amdgcn_s_setprio(SGC_HUB_PRIO);
     __syncthreads();
     float acc = 0.0f;
     for (int r0 = 0; r0 < n_round; r0 += kHubUnroll) {
@@ -425,8 +711,10 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
 #ifndef SGC_HUB_EXPERIMENT
 #define SGC_HUB_EXPERIMENT 0  // timing probes only: 1 = no FMA chain, 2 = no X loads
 #endif
+            if (w == 0) HUB_STAMP(0, r);
             if (w > 0) {
                 if (r + 1 < n_round) store(buf ^ 1, (s + 1) % kHubDepth);
+                if (w == 1) HUB_STAMP(2, r);
                 // ids of round r+D+1 first, so waiting for them (next round)
                 // does not also wait for this round's X loads
                 if (SGC_HUB_EXPERIMENT != 2) {
@@ -435,15 +723,34 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
                 }
             } else if (SGC_HUB_EXPERIMENT != 1) {
                 const int n = min(Sh::kRound, k1 - (k0 + r * Sh::kRound));
-                const f4 *xs = reinterpret_cast<const f4 *>(&gxT[buf][fl * Sh::kStride]);
-                const f4 *vs = reinterpret_cast<const f4 *>(&gv[buf][0]);
                 const int n4 = n >> 2;
                 // LDS reads run kPre batches of four nonzeros ahead of the FMA
                 // chain (a ds_read's ~64-cycle latency otherwise lands on the
                 // chain every four FMAs); reads past n stay inside the padded
                 // row / value buffers (kStride, gv) and are never used.
                 constexpr int kPre = Sh::kPre;
-#if SGC_HUB_SCHED
+#if SGC_HUB_ASM
+                // The chain as one asm loop over four register slots: batch b
+                // (four nonzeros: this lane's X values and their S values,
+                // one ds_read_b128 each) is read four batches before its four
+                // FMAs and waited for with a counted lgkmcnt, so eight LDS
+                // reads stay in flight.  (Left to the compiler, the reads sink
+                // to one batch ahead.)  Same FMA order.  What bounds it is one
+                // wave's LDS read rate: ~35 cycles per 1-KB ds_read_b128 on
+                // gfx950 (scripts/micro/fma_chain.hip: 9-10 cycles per nonzero
+                // alone however deep the ring, vs ~5 for the bare dependent
+                // FMA), ~15 cycles per nonzero beside the loaders' LDS writes
+                // (per-round clock stamps: the chain loop is 95% of each
+                // round; profiles/r02/hub_stamps_*.log).
+                static_assert(kPre >= 4, "the asm chain reads 4 batches ahead");
+                typedef __attribute__((address_space(3))) const float lds_f;
+                uint32_t xa = (uint32_t)(size_t)(lds_f *)(&gxT[buf][fl * Sh::kStride]);
+                uint32_t va = (uint32_t)(size_t)(lds_f *)(&gv[buf][0]);
+                const int iters = n4 >> 2, rem = n4 & 3;
+                hub_chain_asm(acc, xa, va, iters, rem);
+#elif SGC_HUB_SCHED
+                const f4 *xs = reinterpret_cast<const f4 *>(&gxT[buf][fl * Sh::kStride]);
+                const f4 *vs = reinterpret_cast<const f4 *>(&gv[buf][0]);
                 // Ring of 2*kPre slots with compile-time indices: batch b sits
                 // in slot b mod 2kPre, loaded kPre batches before its FMAs, so
                 // no register is copied (a copied load result makes the wave
@@ -483,6 +790,8 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
                         acc = __builtin_fmaf(v[3], x[3], acc);
                     }
 #else
+                const f4 *xs = reinterpret_cast<const f4 *>(&gxT[buf][fl * Sh::kStride]);
+                const f4 *vs = reinterpret_cast<const f4 *>(&gv[buf][0]);
                 f4 xq[kPre], vq[kPre];
 #pragma unroll
                 for (int i = 0; i < kPre; ++i) {
@@ -514,15 +823,22 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
                 const float *xt = &gxT[buf][fl * Sh::kStride];
                 for (int kk = n4 * 4; kk < n; ++kk) acc = __builtin_fmaf(gv[buf][kk], xt[kk], acc);
             }
+            if (w == 0) HUB_STAMP(1, r);
+            if (w == 1) HUB_STAMP(3, r);
             __syncthreads();
         }
     }
     if (w == 0 && seg == 0 && f < F) Y[(int64_t)(row - row_begin) * ldy + f] = acc;
+#if SGC_HUB_STAMPS
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        g_hub_stamp[4][2] = __builtin_amdgcn_s_memtime();
+        g_hub_stamp[4][3] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 namespace {
 
-constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
 struct LaunchArgs {
@@ -618,6 +934,11 @@ hipError_t pooled_event(hipEvent_t *e) {
 #ifndef SGC_HEAVY_U
 #define SGC_HEAVY_U (SGC_PIPE ? 16 : 32)
 #endif
+// Dynamic LDS bytes reserved per light/heavy workgroup (unused by the kernel):
+// caps workgroups per CU (160 KB / bytes), i.e. the gathers in flight per CU.
+// 0 = none.  Set through sgc_set_tuning("light_lds").
+static int g_light_lds = 0;
+
 template <int V, int C>
 hipError_t launch_vc(const LaunchArgs &a) {
     constexpr int U0 = (C * V >= 16) ? 2 : (C * V >= 8) ? 4 : 8;
@@ -627,7 +948,7 @@ hipError_t launch_vc(const LaunchArgs &a) {
     const int64_t waves = (int64_t)a.n_heavy * (C * V / VH) + a.n_rows;
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     dim3 grid((unsigned)blocks, (unsigned)a.slices);
-    hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH>), grid, dim3(kBlock), 0, a.stream,
+    hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH>), grid, dim3(kBlock), g_light_lds, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin, a.n_rows,
                        a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold);
     return hipGetLastError();
@@ -644,6 +965,32 @@ hipError_t dispatch_c(int c, const LaunchArgs &a) {
 }
 
 static int g_max_vec = 4;
+
+// Light kernel choice when 16-B lanes are possible (F rounded up to 4 fits
+// the rows and they are 16-B aligned): 0 = auto -- spmm_rows_kernel when
+// spmm_csr_kernel could not use 16-B lanes itself (F % 4 != 0: Reddit's 602)
+// or the launch is narrower than 128 floats, else spmm_csr_kernel (F = 256 /
+// 500: its one-row 256-float slices measured faster); 2 / 4 = always
+// spmm_rows_kernel with 32 / 16 lanes per row on wide launches; 1 = never.
+// profiles/r02/sweep_rows*.  Set through sgc_set_tuning("rows_per_wave").
+static int g_rows_per_wave = 0;
+
+template <int LB, int VH>
+hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
+    const int R = kWave / LR, SW = LR * 4;
+    const int slices = (F_load + SW - 1) / SW;
+    // heavy sub-chunks per slice: whole 64*VH-float chunks of a slice, or of
+    // the launch's width when it is a single slice
+    const int n_sub = slices > 1 ? SW / (kWave * VH) : (F_load + kWave * VH - 1) / (kWave * VH);
+    const int64_t waves = (int64_t)a.n_heavy * n_sub + (a.n_rows + R - 1) / R;
+    const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    dim3 grid((unsigned)blocks, (unsigned)slices);
+    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, SGC_HEAVY_U>), grid, dim3(kBlock), g_light_lds,
+                       a.stream, a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
+                       a.n_rows, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
+                       a.heavy_threshold);
+    return hipGetLastError();
+}
 
 // Largest per-lane register vector the strides and base pointers allow.
 int pick_vec(int64_t F, int64_t ldx, int64_t ldy, const void *X, const void *Y) {
@@ -699,6 +1046,17 @@ int set_tuning(const char *key, int64_t value) {
         g_hub_first = (int)value;
         return SGC_OK;
     }
+    if (std::string(key) == "rows_per_wave") {
+        SGC_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, SGC_EINVAL,
+                    "rows_per_wave must be 0 (auto), 1, 2 or 4");
+        g_rows_per_wave = (int)value;
+        return SGC_OK;
+    }
+    if (std::string(key) == "light_lds") {
+        SGC_REQUIRE(value >= 0 && value <= 150 * 1024, SGC_EINVAL, "light_lds out of range");
+        g_light_lds = (int)value;
+        return SGC_OK;
+    }
     if (std::string(key) == "max_vec") {
         SGC_REQUIRE(value == 1 || value == 2 || value == 4, SGC_EINVAL, "max_vec must be 1, 2 or 4");
         g_max_vec = (int)value;
@@ -711,6 +1069,8 @@ int set_tuning(const char *key, int64_t value) {
 int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "slice_floats") return g_slice_floats;
     if (key && std::string(key) == "max_vec") return g_max_vec;
+    if (key && std::string(key) == "rows_per_wave") return g_rows_per_wave;
+    if (key && std::string(key) == "light_lds") return g_light_lds;
     if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
     if (key && std::string(key) == "hub_priority") return g_hub_priority;
     if (key && std::string(key) == "hub_first") return g_hub_first;
@@ -720,7 +1080,7 @@ int64_t get_tuning(const char *key) {
 int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                 int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
                 int64_t ldy, int64_t F, const int32_t *heavy_rows, int64_t n_heavy,
-                int64_t n_hub, int32_t heavy_threshold, hipStream_t stream) {
+                int64_t n_hub, int32_t heavy_threshold, uint32_t flags, hipStream_t stream) {
     SGC_REQUIRE(row_ptr && col_idx && val && X && Y, SGC_EINVAL, "spmm: null pointer");
     SGC_REQUIRE(row_begin >= 0 && row_end >= row_begin && row_end < INT32_MAX, SGC_ERANGE,
                 "spmm: bad row range [%lld, %lld)", (long long)row_begin, (long long)row_end);
@@ -735,6 +1095,13 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         heavy_threshold = INT32_MAX;  // no plan: every row is a light item
     }
     n_hub = std::max<int64_t>(0, std::min<int64_t>(n_hub, n_heavy));
+    if (flags & SGC_SPMM_NO_HUB) {  // hub rows are launched separately (SGC_SPMM_HUB_ONLY)
+        heavy_rows += n_hub;
+        n_heavy -= n_hub;
+        n_hub = 0;
+    }
+    const bool hub_only = (flags & SGC_SPMM_HUB_ONLY) != 0;
+    if (hub_only && n_hub == 0) return SGC_OK;
     SideStream *side = nullptr;
     std::unique_lock<std::mutex> side_lock;
     std::unique_lock<std::mutex> timing_lock(g_timing_mu);
@@ -751,12 +1118,15 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         const int hc = g_hub_chunk ? g_hub_chunk : (lines && F <= 192 ? 32 : 64);
         const int n_chunks = (int)((F + hc - 1) / hc);
         SGC_REQUIRE(n_hub * n_chunks < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many hub items");
-        SGC_HIP_CHECK(side_stream(&side));
-        side_lock = std::unique_lock<std::mutex>(side->mu);
-        SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
-        SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
-        hipStream_t hs = g_hub_first ? stream : side->s;
-        light_stream = g_hub_first ? side->s : stream;
+        hipStream_t hs = stream;  // HUB_ONLY: on the caller's stream, nothing else
+        if (!hub_only) {
+            SGC_HIP_CHECK(side_stream(&side));
+            side_lock = std::unique_lock<std::mutex>(side->mu);
+            SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
+            SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
+            hs = g_hub_first ? stream : side->s;
+            light_stream = g_hub_first ? side->s : stream;
+        }
         if (timing) {
             SGC_HIP_CHECK(pooled_event(&tl.h0));
             SGC_HIP_CHECK(pooled_event(&tl.h1));
@@ -774,32 +1144,77 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         if (timing) SGC_HIP_CHECK(hipEventRecord(tl.h1, hs));
         heavy_rows += n_hub;
         n_heavy -= n_hub;
+        if (hub_only) {
+            if (timing) {  // no light kernel: an empty light interval
+                SGC_HIP_CHECK(pooled_event(&tl.l0));
+                SGC_HIP_CHECK(pooled_event(&tl.l1));
+                SGC_HIP_CHECK(hipEventRecord(tl.l0, hs));
+                SGC_HIP_CHECK(hipEventRecord(tl.l1, hs));
+                g_timed.push_back(tl);
+            }
+            return SGC_OK;
+        }
     }
-
-    const int V = pick_vec(F, ldx, ldy, X, Y);
-    const int chunks_total = (int)((F + kWave * V - 1) / (kWave * V));
-    const int cmax = max_chunks(V);
-    int C = g_slice_floats > 0 ? std::max(1, g_slice_floats / (kWave * V)) : cmax;
-    C = std::min(C, std::min(cmax, chunks_total));
-    const int slices = (chunks_total + C - 1) / C;
-    const int64_t waves = n_heavy * (int64_t)C * V + n_rows;  // upper bound (VH >= 1)
-    SGC_REQUIRE(waves < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many work items");
-    SGC_REQUIRE(slices < 65536, SGC_ERANGE, "spmm: too many feature slices");
 
     LaunchArgs a{row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)n_rows, (int)F,
-                 heavy_rows, (int)n_heavy, heavy_threshold, slices, light_stream};
-    if (timing) {
-        SGC_HIP_CHECK(pooled_event(&tl.l0));
-        SGC_HIP_CHECK(pooled_event(&tl.l1));
-        SGC_HIP_CHECK(hipEventRecord(tl.l0, light_stream));
+                 heavy_rows, (int)n_heavy, heavy_threshold, 0, light_stream};
+    // 16-B lanes over F rounded up to 4 columns: X rows must be 16-B aligned
+    // and readable that far (flag SGC_SPMM_X_PADDED unless F % 4 == 0)
+    const int64_t F4 = (F + 3) / 4 * 4;
+    const uintptr_t xa = reinterpret_cast<uintptr_t>(X), ya = reinterpret_cast<uintptr_t>(Y);
+    const bool v4_ok = ldx % 4 == 0 && xa % 16 == 0 && F4 <= ldx && F4 >= 32 &&
+                       (F4 == F || (flags & SGC_SPMM_X_PADDED));
+    const bool csr_v4 = F % 4 == 0 && pick_vec(F, ldx, ldy, X, Y) == 4;
+    const bool rows_kernel = v4_ok && g_rows_per_wave != 1 &&
+                             (g_rows_per_wave > 1 || !csr_v4 || F4 < 128);
+    hipError_t e = hipSuccess;
+    if (rows_kernel) {
+        const int vec_store = ldy % 4 == 0 && ya % 16 == 0 && F4 <= ldy &&
+                              (F4 == F || (flags & SGC_SPMM_Y_PADDED));
+        // lanes per row: the launch's width in 4-float lanes when it fits a
+        // wave's half or less (one slice), else 32 (or 16 when forced)
+        int LR = F4 >= 128 ? (g_rows_per_wave == 4 ? 16 : 32) : (int)(F4 / 4);
+        if (LR > 32) LR = 32;
+        const int SW = LR * 4;
+        const bool multi = F4 > SW;
+        const bool vh2 = F % 2 == 0 && ldx % 2 == 0 && ldy % 2 == 0 && xa % 8 == 0 &&
+                         ya % 8 == 0 && (!multi || SW % (kWave * 2) == 0);
+        SGC_REQUIRE(n_heavy * 8 + n_rows < (int64_t)INT32_MAX, SGC_ERANGE,
+                    "spmm: too many work items");
+        if (timing) {
+            SGC_HIP_CHECK(pooled_event(&tl.l0));
+            SGC_HIP_CHECK(pooled_event(&tl.l1));
+            SGC_HIP_CHECK(hipEventRecord(tl.l0, light_stream));
+        }
+        if (LR >= 16)
+            e = vh2 ? launch_rows<16, 2>(a, (int)F4, LR, vec_store)
+                    : launch_rows<16, 1>(a, (int)F4, LR, vec_store);
+        else
+            e = vh2 ? launch_rows<8, 2>(a, (int)F4, LR, vec_store)
+                    : launch_rows<8, 1>(a, (int)F4, LR, vec_store);
+    } else {
+        const int V = pick_vec(F, ldx, ldy, X, Y);
+        const int chunks_total = (int)((F + kWave * V - 1) / (kWave * V));
+        const int cmax = max_chunks(V);
+        int C = g_slice_floats > 0 ? std::max(1, g_slice_floats / (kWave * V)) : cmax;
+        C = std::min(C, std::min(cmax, chunks_total));
+        const int slices = (chunks_total + C - 1) / C;
+        const int64_t waves = n_heavy * (int64_t)C * V + n_rows;  // upper bound (VH >= 1)
+        SGC_REQUIRE(waves < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many work items");
+        SGC_REQUIRE(slices < 65536, SGC_ERANGE, "spmm: too many feature slices");
+        a.slices = slices;
+        if (timing) {
+            SGC_HIP_CHECK(pooled_event(&tl.l0));
+            SGC_HIP_CHECK(pooled_event(&tl.l1));
+            SGC_HIP_CHECK(hipEventRecord(tl.l0, light_stream));
+        }
+        if (V == 4)
+            e = dispatch_c<4, max_chunks(4)>(C, a);
+        else if (V == 2)
+            e = dispatch_c<2, max_chunks(2)>(C, a);
+        else
+            e = dispatch_c<1, max_chunks(1)>(C, a);
     }
-    hipError_t e;
-    if (V == 4)
-        e = dispatch_c<4, max_chunks(4)>(C, a);
-    else if (V == 2)
-        e = dispatch_c<2, max_chunks(2)>(C, a);
-    else
-        e = dispatch_c<1, max_chunks(1)>(C, a);
     SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "spmm launch failed: %s", hipGetErrorString(e));
     if (timing) {
         SGC_HIP_CHECK(hipEventRecord(tl.l1, light_stream));
@@ -811,6 +1226,15 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     }
     return SGC_OK;
 }
+
+#if SGC_HUB_STAMPS
+extern "C" int sgc_debug_hub_stamps(unsigned long long *host, int64_t n) {
+    const int64_t cap = 5 * (int64_t)kStampRounds;
+    SGC_HIP_CHECK(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_hub_stamp),
+                                      sizeof(unsigned long long) * (n < cap ? n : cap)));
+    return SGC_OK;
+}
+#endif
 
 int timing_enable(int on) {
     std::lock_guard<std::mutex> lock(g_timing_mu);

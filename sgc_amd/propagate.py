@@ -55,6 +55,9 @@ class Plan(NamedTuple):
 
 NO_PLAN = Plan(None, 0, 0, 0)
 
+SPMM_X_PADDED = 1  # sgc_spmm_csr_f32_ex flags (include/sgc_amd.h)
+SPMM_Y_PADDED = 2
+
 STATUS_ROWS_SORTED = 1
 STATUS_COLS_ASCENDING = 2
 STATUS_OUT_OF_RANGE = 4
@@ -396,13 +399,16 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
             src, nxt = bufs[0][:, :F], 1 % len(bufs)
         for h in range(K):
             dst = out if h == K - 1 else bufs[nxt][:, :F]
+            # the engine's own buffers may be read / written in their pad columns
+            flags = ((SPMM_X_PADDED if src is not X else 0) |
+                     (SPMM_Y_PADDED if dst is not out else 0))
             if hop_hook:
                 hop_hook("start", h)
-            _lib.check(lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
-                                            _lib.ptr(csr.val), 0, n, _lib.ptr(src), src.stride(0),
-                                            _lib.ptr(dst), dst.stride(0), F, _lib.ptr(pl.rows),
-                                            pl.n_heavy, pl.n_hub, pl.threshold, stream),
-                       "spmm_csr_f32")
+            _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
+                                               _lib.ptr(csr.val), 0, n, _lib.ptr(src),
+                                               src.stride(0), _lib.ptr(dst), dst.stride(0), F,
+                                               _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub,
+                                               pl.threshold, flags, stream), "spmm_csr_f32")
             if hop_hook:
                 hop_hook("end", h)
             src, nxt = dst, nxt ^ 1

@@ -54,20 +54,24 @@ def test_tiny_cases_sgc_precompute_bit_exact(tiny_cases):
             assert bits_equal(out.cpu().numpy(), c[key]), (name, K)
 
 
+@pytest.mark.parametrize("rows_per_wave", [0, 1, 2, 4])
 @pytest.mark.parametrize("hub_chunk", [0, 32, 64])
 @pytest.mark.parametrize("threshold,hub", [(0, 0), (1, 7), (7, 7), (63, 500), (0, 10**9),
                                            (10**9, 10**9), (2048, 4096)])
-def test_heavy_split_schedule_never_changes_bits(tiny_cases, threshold, hub, hub_chunk):
+def test_heavy_split_schedule_never_changes_bits(tiny_cases, threshold, hub, hub_chunk,
+                                                 rows_per_wave):
     """Every row a hub (0, 0), every row heavy (0, inf) .. no heavy rows, hub
-    kernel on 32- or 64-feature chunks: same bits."""
+    kernel on 32- or 64-feature chunks, light rows one / two / four per wave
+    (spmm_csr_kernel / spmm_rows_kernel): same bits."""
     from sgc_amd import _lib
-    from sgc_amd.propagate import DeviceCSR, propagate
     lib = _lib.load()
     _lib.check(lib.sgc_set_tuning(b"hub_chunk", hub_chunk), "set_tuning")
+    _lib.check(lib.sgc_set_tuning(b"rows_per_wave", rows_per_wave), "set_tuning")
     try:
         _schedule_cases(tiny_cases, threshold, hub)
     finally:
         lib.sgc_set_tuning(b"hub_chunk", 0)
+        lib.sgc_set_tuning(b"rows_per_wave", 0)
 
 
 def _schedule_cases(tiny_cases, threshold, hub):
@@ -94,19 +98,25 @@ def test_no_plan_path(tiny_cases):
 
 @pytest.mark.parametrize("native", [False, True])
 @pytest.mark.parametrize("ld_extra", [0, 38, 3])
-def test_propagate_layouts_and_native_loop(tiny_cases, native, ld_extra):
+@pytest.mark.parametrize("name", ["norm_n48_F602", "norm_n48_F65", "norm_n48_F130"])
+def test_propagate_layouts_and_native_loop(tiny_cases, native, ld_extra, name):
     """Python hop loop and the C ABI loop (sgc_propagate_f32), with inputs
-    needing the 128-B re-layout (ld 602 / 605) and not (ld 640)."""
+    needing the 128-B re-layout (ld F / F+3) and not (ld F+38 when that is a
+    multiple of 32), at F = 602 / 65 / 130 (pad columns up to a multiple of 4
+    computed inside the engine's buffers, never in the caller's)."""
     from sgc_amd.propagate import DeviceCSR, propagate
-    c = tiny_cases["norm_n48_F602"]
+    c = tiny_cases[name]
+    F = c["X"].shape[1]
     csr = DeviceCSR.from_torch(coo_cuda(c))
     X = torch.from_numpy(c["X"]).to(DEV)
-    buf = torch.full((X.shape[0], 602 + ld_extra), float("nan"), device=DEV)
-    buf[:, :602] = X
+    buf = torch.full((X.shape[0], F + ld_extra), float("nan"), device=DEV)
+    buf[:, :F] = X
     for K in (0, 1, 2, 3):
-        out = propagate(csr, buf[:, :602], K, native_loop=native)
+        out = torch.full((X.shape[0], F + 5), float("nan"), device=DEV)
+        got = propagate(csr, buf[:, :F], K, out=out[:, :F], native_loop=native)
         torch.cuda.synchronize()
-        assert bits_equal(out.cpu().numpy(), c[f"Y{K}"]), (K, native, ld_extra)
+        assert bits_equal(got.cpu().numpy(), c[f"Y{K}"]), (K, native, ld_extra)
+        assert torch.isnan(out[:, F:]).all()  # nothing written past F in the caller's rows
 
 
 def test_row_slices_and_strides(tiny_cases):
@@ -279,6 +289,34 @@ def test_long_hub_rows_bit_exact(oracle, F, hub_chunk):
         assert bits_equal(out.cpu().numpy(), want)
     finally:
         lib.sgc_set_tuning(b"hub_chunk", 0)
+
+
+@pytest.mark.parametrize("F", [32, 36, 44, 76, 96, 100, 124, 152])
+def test_narrow_launches_rows_kernel(oracle, F):
+    """Feature widths below a slice (the feature partition's column blocks,
+    the row partition's narrow groups): spmm_rows_kernel packs 64 // (F/4)
+    rows into a wave.  Heavy rows (threshold 40) and hub rows (500) on the
+    same launch; X in 128-B rows so hop 1 also takes 16-B lanes."""
+    from sgc_amd import graphs
+    from sgc_amd.propagate import DeviceCSR, propagate
+    rng = np.random.default_rng(F)
+    n = 3000
+    lo = np.concatenate([np.zeros(900, np.int64), np.full(300, 7, np.int64),
+                         rng.integers(0, n, 15000)])
+    hi = np.concatenate([np.arange(100, 1000), np.arange(1000, 1300), rng.integers(0, n, 15000)])
+    keep = lo != hi
+    a, b = np.minimum(lo, hi)[keep], np.maximum(lo, hi)[keep]
+    key = np.unique(a * n + b)
+    S = graphs.aug_norm_csr_from_pairs(n, key // n, key % n)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    want = oracle.propagate(S.row_ptr, S.col_idx, S.val, X, 2)
+    csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val)
+    Xd = torch.zeros((n, (F + 31) // 32 * 32), device=DEV)[:, :F]
+    Xd.copy_(torch.from_numpy(X))
+    for th, hub in ((40, 500), (10**9, 10**9)):
+        out = propagate(csr, Xd, 2, threshold=th, hub_threshold=hub)
+        torch.cuda.synchronize()
+        assert bits_equal(out.cpu().numpy(), want), (F, th, hub)
 
 
 def test_fused_xent_rejects_bad_labels():
