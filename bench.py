@@ -9,9 +9,11 @@ synthetic Reddit-shape graph (232,965 nodes, 11,606,919 undirected edges,
 nnz(S) = 23,446,803, F = 602, K = 2), inputs resident in HBM.
 A "step" = one full K-hop propagation.  N > 1 (sgc_amd.distributed), total
 work fixed, so scaling is "strong":
-  --partition rows (default)  S row-partitioned (equal-row blocks, SURVEY.md
-                8(e)); RCCL all-gather of X_k after each hop that feeds another,
-                pipelined in feature groups
+  --partition rows (default)  S row-partitioned (nnz-balanced row blocks,
+                SURVEY.md 8(e)); RCCL all-gather of X_k after each hop that feeds
+                another, pipelined in feature groups, hub rows on their own streams
+  --partition tiles  R x C: row blocks x --col-blocks feature blocks; the
+                per-hop all-gather runs within each feature block's R ranks
   --partition features  each rank runs all K hops on its block of feature
                 columns over the full S, no exchange between hops
   --output sharded (default)  each rank ends with its row block of X_K
@@ -347,7 +349,7 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
 
     def bracket(fn, nbytes):
         def run(*a, **k):
-            if not timing["on"]:
+            if not timing["on"] or "hub" in a[3:]:  # time the light launches (rank 0's rows)
                 return fn(*a, **k)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
@@ -383,31 +385,52 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
                f"{exch}; output {output}")
         unit = f"rank 0's SpMM launches, {int(fb[1] - fb[0])} feature columns"
     else:
-        from sgc_amd.distributed import RowPartitionedPropagator, _default_spmm, make_shard
-        shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
+        from sgc_amd.distributed import (RowPartitionedPropagator, TiledPropagator,
+                                         _default_spmm, feature_bounds, make_shard)
 
-        def launch_bytes(sh, X, out):
+        def launch_bytes(sh, X, out, *rest):
             w = X.shape[1]
             return 4 * (sh.rows + 1) + 8 * sh.nnz + 4 * w * n + 4 * w * sh.rows
 
+        C = args.col_blocks if args.partition == "tiles" else 1
         auto = args.group_floats == "auto"
-        prop = RowPartitionedPropagator(shard, spmm_fn=bracket(_default_spmm, launch_bytes),
-                                        group_floats=224 if auto else int(args.group_floats),
-                                        host_staging=staging)
+        gf0 = 128 if auto else int(args.group_floats)
+        spmm_fn = bracket(_default_spmm, launch_bytes)
+        if C > 1:
+            if output != "sharded":
+                raise SystemExit("--partition tiles: output sharded only")
+            tp = TiledPropagator(S.row_ptr, S.col_idx, S.val, rank, world, C, dev,
+                                 group_floats=gf0, host_staging=staging, spmm_fn=spmm_fn)
+            prop, shard = tp.prop, tp.shard
+            fb, _ = feature_bounds(F, C)
+            Xa = X0[:, int(fb[tp.j]):int(fb[tp.j + 1])]
+        else:
+            shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
+            prop = RowPartitionedPropagator(shard, spmm_fn=spmm_fn, group_floats=gf0,
+                                            host_staging=staging)
+            tp, Xa = None, X0
         tuned = ""
-        if auto:  # untimed setup, like the plans: every rank picks the same width
-            tt = prop.autotune(X0, K, output=output)
+        if auto and shard.world_size > 1:  # untimed setup, like the plans
+            tt = prop.autotune(Xa, K, output="sharded" if C > 1 else output)
             tuned = " (autotuned: " + ", ".join(f"{g}: {t * 1e3:.2f} ms"
                                                 for g, t in tt.items()) + ")"
         gf = prop.group_floats
         exch = ("all-gather of X_k after each hop but the last" if output == "sharded" else
                 "all-gather of X_k after every hop")
-        par = (f"row-partition x{world} (equal-row blocks) + {backend} {exch}, pipelined in "
-               f"{gf}-float feature groups{tuned}; output {output}")
+        if C > 1:
+            par = (f"2-D tiles {world // C} nnz-balanced row blocks x {C} feature blocks + "
+                   f"{backend} {exch} within each feature block's {world // C} ranks, pipelined "
+                   f"in {gf}-float groups{tuned}, + one all-gather of the {C} tiles of each row "
+                   f"block; output sharded")
+        else:
+            par = (f"row-partition x{world} (nnz-balanced row blocks) + {backend} {exch}, "
+                   f"pipelined in {gf}-float feature groups{tuned}; output {output}")
         unit = f"rank 0's {shard.rows} rows ({shard.nnz} nnz)"
     out = torch.empty((n, F), device=dev) if output == "replicated" else None
 
     def step():
+        if args.partition == "tiles" and tp is not None:
+            return tp.propagate(X0, K, output="sharded")
         return prop.propagate(X0, K, out=out, output=output)
     return step, par, unit
 
@@ -428,13 +451,16 @@ def main():
     ap.add_argument("--hub-threshold", type=int, default=None, help="hub-row threshold")
     ap.add_argument("--group-floats", default="auto",
                     help="N>1 rows: feature-group width of the compute/all-gather pipeline "
-                         "(an integer, or auto = timed on this node among 224/304/160)")
+                         "(an integer, or auto = timed on this node among 128/256/224)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged rehearsal of the N>1 path (ranks may share a GPU)")
     ap.add_argument("--distributed-path", action="store_true",
                     help="run the N>1 path even at N=1 (exercises RCCL on one GPU)")
-    ap.add_argument("--partition", default="rows", choices=["rows", "features"],
-                    help="N>1: split the rows of S (per-hop all-gather) or the feature columns")
+    ap.add_argument("--partition", default="rows", choices=["rows", "tiles", "features"],
+                    help="N>1: split the rows of S (per-hop all-gather), rows x feature blocks "
+                         "(tiles, --col-blocks), or the feature columns")
+    ap.add_argument("--col-blocks", type=int, default=2,
+                    help="N>1 tiles: feature blocks C (P = R x C)")
     ap.add_argument("--output", default="sharded", choices=["sharded", "replicated"],
                     help="N>1: each rank keeps its row block of X_K, or all ranks get all of it")
     ap.add_argument("--chunks", type=int, default=4,
@@ -519,7 +545,7 @@ def main():
                                 on_stop=lambda: tm.update(on=False))
     launch_ms = [s.elapsed_time(e) for s, e in tm["pairs"]]
     alt = None
-    if args.alt_steps > 0:
+    if args.alt_steps > 0 and args.partition != "tiles":
         alt_mode = "replicated" if args.output == "sharded" else "sharded"
         alt_step, alt_par, _ = build_dist_step(args, S, X0, dev, rank, world, K, alt_mode,
                                                {"on": False})

@@ -49,16 +49,44 @@ def nnz_balanced_bounds(row_ptr, world_size):
     return np.concatenate([[0], inner, [n]]).astype(np.int64)
 
 
+def equal_row_bounds(n, world_size):
+    """r_p = min(p * ceil(n/P), n): equal blocks, the last one shorter."""
+    B = max(1, -(-n // world_size))
+    return np.minimum(np.arange(world_size + 1, dtype=np.int64) * B, n)
+
+
+def partition_bounds(row_ptr, world_size, balance="nnz"):
+    """Row blocks of the row partition: "nnz" (equal nonzeros, the default:
+    power-law hubs and skewed degree ranges do not unbalance the ranks) or
+    "rows" (equal rows)."""
+    if balance == "nnz":
+        return nnz_balanced_bounds(row_ptr, world_size)
+    if balance == "rows":
+        return equal_row_bounds(len(row_ptr) - 1, world_size)
+    raise ValueError(f"balance must be 'nnz' or 'rows', not {balance!r}")
+
+
+def gathered_index(bounds, B, j):
+    """Row of global node j in the gathered [P*B, F] exchange buffer: block p
+    = the rank owning j lands at rows [p*B, p*B + rows_p)."""
+    j = np.asarray(j, dtype=np.int64)
+    p = np.searchsorted(bounds, j, side="right") - 1
+    return j - bounds[p] + p * B
+
+
 @dataclass
 class ShardCSR:
-    """One rank's rows of S (row_ptr rebased to 0, global column indices)."""
+    """One rank's rows of S (row_ptr rebased to 0).  Two column-index arrays:
+    global node ids (hop 1 reads the caller's X_0) and rows of the gathered
+    exchange buffer (later hops; identical when the blocks have equal rows)."""
     rank: int
     world_size: int
     bounds: np.ndarray      # [P+1] row boundaries
     row_ptr: torch.Tensor   # int32 [rows+1]
-    col_idx: torch.Tensor   # int32 [nnz_local]
+    col_idx: torch.Tensor   # int32 [nnz_local], global ids
     val: torch.Tensor       # float32 [nnz_local]
     n: int
+    col_gathered: Optional[torch.Tensor] = None  # int32 [nnz_local], gathered-buffer rows
 
     @property
     def row_begin(self):
@@ -78,55 +106,98 @@ class ShardCSR:
 
     @property
     def block(self):
-        return max(1, -(-self.n // self.world_size))
+        """Rows per block of the gathered buffer: the largest rank's rows."""
+        return max(1, int(np.max(np.diff(self.bounds))))
+
+    @property
+    def gathered_rows(self):
+        return self.world_size * self.block
+
+    @property
+    def identity_layout(self):
+        """Global row j sits at row j of the gathered buffer (equal blocks)."""
+        B = self.block
+        return all(int(self.bounds[p]) == min(p * B, self.n) for p in range(self.world_size + 1))
 
 
-def equal_row_bounds(n, world_size):
-    """r_p = min(p * ceil(n/P), n): equal blocks, the last one shorter."""
-    B = max(1, -(-n // world_size))
-    return np.minimum(np.arange(world_size + 1, dtype=np.int64) * B, n)
-
-
-def make_shard(row_ptr, col_idx, val, rank, world_size, device):
+def make_shard(row_ptr, col_idx, val, rank, world_size, device, balance="nnz"):
     """Slice the host CSR (numpy) for `rank` and move it to `device`."""
     row_ptr = np.asarray(row_ptr, dtype=np.int64)
-    n = row_ptr.shape[0] - 1
-    bounds = equal_row_bounds(n, world_size)
+    bounds = partition_bounds(row_ptr, world_size, balance)
+    B = max(1, int(np.max(np.diff(bounds))))
     r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
     k0, k1 = int(row_ptr[r0]), int(row_ptr[r1])
+    cols = np.asarray(col_idx[k0:k1]).astype(np.int64)
+    gcols = gathered_index(bounds, B, cols)
+    if world_size * B >= 2**31:
+        raise ValueError("gathered exchange buffer exceeds int32 row ids")
 
     def t(a, dt):
         return torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dt)
 
-    return ShardCSR(rank, world_size, bounds, t(row_ptr[r0:r1 + 1] - k0, torch.int32),
-                    t(np.asarray(col_idx[k0:k1]), torch.int32),
-                    t(np.asarray(val[k0:k1]), torch.float32), n)
+    c = t(cols, torch.int32)
+    cg = c if np.array_equal(gcols, cols) else t(gcols, torch.int32)
+    return ShardCSR(rank, world_size, bounds, t(row_ptr[r0:r1 + 1] - k0, torch.int32), c,
+                    t(np.asarray(val[k0:k1]), torch.float32), int(row_ptr.shape[0] - 1), cg)
 
 
-def _default_spmm(shard: ShardCSR, X, out):
-    from .propagate import DeviceCSR, spmm
-    cache = shard.__dict__.setdefault("_csr_by_cols", {})  # hop 1 reads N rows, later P*B
-    csr = cache.get(X.shape[0])
+def _default_spmm(shard: ShardCSR, X, out, layout="input", part="all"):
+    """This rank's rows of S.X through the product engine (HIP on ROCm
+    tensors, the CPU twin on CPU tensors).  layout: "input" = X is the
+    caller's [N, F] X_0 (global column ids), "gathered" = X is the [P*B, F]
+    exchange buffer.  part: "all", or the split launch of the multi-GPU
+    pipeline -- "light" (every row but the hub rows) and "hub" (only them).
+    On the GPU each distinct launch is prepared once (SpmmLaunch) and
+    replayed with the current stream: the pipeline's per-step host time
+    stays far below its GPU time."""
+    from . import _lib
+    from .propagate import SPMM_HUB_ONLY, SPMM_NO_HUB, DeviceCSR, SpmmLaunch, spmm
+    cache = shard.__dict__.setdefault("_csr_by_layout", {})
+    csr = cache.get(layout)
     if csr is None:
-        csr = DeviceCSR(shard.rows, X.shape[0], shard.row_ptr, shard.col_idx, shard.val)
-        cache[X.shape[0]] = csr
-    return spmm(csr, X, 0, shard.rows, out=out)
+        cols = shard.col_idx if layout == "input" else shard.col_gathered
+        n_cols = shard.n if layout == "input" else shard.gathered_rows
+        csr = DeviceCSR(shard.rows, n_cols, shard.row_ptr, cols, shard.val)
+        cache[layout] = csr
+    flags = {"all": 0, "light": SPMM_NO_HUB, "hub": SPMM_HUB_ONLY}[part]
+    if not X.is_cuda:
+        return spmm(csr, X, 0, shard.rows, out=out, flags=flags)
+    launches = shard.__dict__.setdefault("_launches", {})
+    key = (layout, part, X.data_ptr(), tuple(X.shape), X.stride(0), out.data_ptr(),
+           tuple(out.shape), out.stride(0))
+    fn = launches.get(key)
+    if fn is None:
+        if len(launches) > 256:
+            launches.clear()
+        fn = launches[key] = SpmmLaunch(csr, X, out, 0, shard.rows, flags)
+    fn(_lib.stream_handle(X.device))
+    return out
 
 
 class RowPartitionedPropagator:
     """X_K = S^K X_0 with S row-sharded over the process group.
 
     X_0 must be the full [N, F] features on every rank (inputs replicated, as
-    the reference loads them); the result is the full X_K on every rank.
-    `spmm_fn(shard, X, out)` computes the rank's rows of S.X; the default is the
-    HIP kernel (tests inject the CPU oracle to exercise the exchange logic over
-    gloo).  On the GPU the feature width is padded to a multiple of 32 floats
-    inside the engine (128-B rows in every exchanged buffer; the padding
-    columns are computed and never returned)."""
+    the reference loads them).  Each hop computes this rank's rows of S.X_k
+    with the HIP kernel (global column ids for hop 1, gathered-buffer rows
+    after) and all-gathers them into the [P*B, F] exchange buffer the next
+    hop reads (B = the largest block; blocks are nnz-balanced).
+
+    Pipeline per hop (ROCm tensors): the features are processed in groups;
+    group g runs as two launches -- every row but the hub rows on the
+    caller's stream, the hub rows (long LDS-staged FMA chains) on a hub
+    stream -- and group g's all-gather is issued from a comm stream once
+    both are done, so the next group's light launch never waits for the hub
+    chains and the exchange of group g overlaps the compute of group g+1 and
+    the next hop's groups < g.  Bit-exact: every row is still one FMA chain
+    per element in CSR order.
+
+    `spmm_fn(shard, X, out, layout, part)` computes the rank's rows; the
+    default is the product engine (tests inject the CPU oracle)."""
 
     def __init__(self, shard: ShardCSR, group=None, spmm_fn: Optional[Callable] = None,
-                 group_floats: int = 224, host_staging: bool = False,
-                 pad_input: Optional[bool] = None):
+                 group_floats: int = 128, host_staging: bool = False,
+                 pad_input: Optional[bool] = None, split_hubs: bool = True):
         self.shard = shard
         # Re-lay X_0 into 128-B rows before hop 1?  The copy (all N rows, ~0.2 ms
         # at Reddit shape) beats reading 8-B aligned rows only while this rank's
@@ -138,7 +209,11 @@ class RowPartitionedPropagator:
         self.group_floats = max(2, int(group_floats) // 2 * 2)  # 8-B aligned groups
         # rehearsal only: gather device buffers through host copies (gloo)
         self.host_staging = host_staging
+        self.split_hubs = split_hubs
         self._bufs = {}
+        self._streams = None
+        self._hub_streams = []
+        self._event_pool = {}
 
     def _buf(self, key, shape, like):
         b = self._bufs.get(key)
@@ -148,6 +223,9 @@ class RowPartitionedPropagator:
         return b
 
     def _all_gather(self, full, loc):
+        if self.shard.world_size == 1:  # the exchange of one rank is a copy
+            full.copy_(loc)
+            return None
         if not self.host_staging:
             return dist.all_gather_into_tensor(full, loc, group=self.group, async_op=True)
         h_full = torch.empty(full.shape, dtype=full.dtype)
@@ -155,7 +233,7 @@ class RowPartitionedPropagator:
         full.copy_(h_full)
         return None
 
-    def autotune(self, X0, K, output="sharded", candidates=(224, 304, 160), reps=2):
+    def autotune(self, X0, K, output="sharded", candidates=(128, 256, 224), reps=2):
         """Pick group_floats by timing whole propagations (collective: every
         rank must call it with the same arguments).  The best grouping depends
         on the exchange rate, which only the node knows: with a fast all-gather
@@ -190,6 +268,46 @@ class RowPartitionedPropagator:
         self._bufs.clear()
         return times
 
+    def _compute(self, X, out, layout, split, key=None):
+        """One group's local SpMM: (light event, hub event) on the GPU when the
+        launch is split, else (None, None) after one launch."""
+        if not split:
+            if self.shard.rows:
+                self.spmm_fn(self.shard, X, out, layout, "all")
+            return None, None
+        main = torch.cuda.current_stream(X.device)
+        hub_s = self._hub_stream(key[1], X.device)
+        ready, ev_l, ev_h = self._events(key)
+        ready.record(main)
+        if self.shard.rows:
+            self.spmm_fn(self.shard, X, out, layout, "light")
+        ev_l.record(main)
+        hub_s.wait_event(ready)
+        with torch.cuda.stream(hub_s):
+            if self.shard.rows:
+                self.spmm_fn(self.shard, X, out, layout, "hub")
+        ev_h.record(hub_s)
+        return ev_l, ev_h
+
+    def _hub_stream(self, gi, device):
+        """One stream per feature group for its hub rows: the hub kernels of a
+        hop's groups run concurrently (each is bounded by its longest row's
+        FMA chain, ~0.3 ms for the 47,857-nonzero row), not one after another."""
+        hs = self._hub_streams
+        while len(hs) <= gi:
+            hs.append(torch.cuda.Stream(device=device))
+        return hs[gi]
+
+    def _events(self, key):
+        """(input ready, light done, hub done) events of one launch slot, made
+        once and re-recorded every step (a wait enqueued earlier keeps the
+        state it saw)."""
+        ev = self._event_pool.get(key)
+        if ev is None:
+            ev = self._event_pool[key] = (torch.cuda.Event(), torch.cuda.Event(),
+                                          torch.cuda.Event())
+        return ev
+
     def propagate(self, X0, K, out=None, output="replicated"):
         """output="replicated": the full X_K [N, F] on every rank (one more
         all-gather after the last hop).  output="sharded": this rank's rows
@@ -202,6 +320,10 @@ class RowPartitionedPropagator:
             raise ValueError(f"output must be 'replicated' or 'sharded', not {output!r}")
         if K <= 0:
             return X0 if output == "replicated" else X0[s.row_begin:s.row_end]
+        split = X0.is_cuda and self.split_hubs and not self.host_staging
+        if split and self._streams is None:
+            self._streams = (torch.cuda.Stream(device=X0.device),
+                             torch.cuda.Stream(device=X0.device))
         Fp = F
         if X0.is_cuda:
             from . import _lib
@@ -214,8 +336,12 @@ class RowPartitionedPropagator:
                     _lib.ptr(X0), X0.stride(0), _lib.ptr(Xa), Fp, n, F,
                     _lib.stream_handle(X0.device)), "pad_rows_f32")
                 X0 = Xa
-        groups = [(a, min(Fp, a + self.group_floats)) for a in range(0, Fp, self.group_floats)]
+        # one group on a single rank: nothing to overlap, and each extra group
+        # re-reads the CSR and adds a launch tail (+35% at world 1, r01)
+        gf = self.group_floats if s.world_size > 1 else Fp
+        groups = [(a, min(Fp, a + gf)) for a in range(0, Fp, gf)]
         src = [X0[:, a:min(b, X0.shape[1])] for a, b in groups]  # unpadded: last one narrower
+        layout = "input"
         works = [None] * len(groups)
         if output == "sharded":
             K_ex = K - 1  # hops whose output is exchanged
@@ -223,6 +349,7 @@ class RowPartitionedPropagator:
                 out = torch.empty((s.rows, F), dtype=torch.float32, device=X0.device)
         else:
             K_ex = K
+        PB = s.gathered_rows
         for h in range(K_ex):
             par = h & 1
             new_works, gathered = [], []
@@ -230,30 +357,144 @@ class RowPartitionedPropagator:
                 if works[gi] is not None:
                     works[gi].wait()  # this hop's input group has arrived (stream wait)
                 loc = self._buf(("local", par, gi), (s.block, b - a), X0)
-                if s.rows:
-                    self.spmm_fn(s, src[gi], loc[:s.rows, :src[gi].shape[1]])
-                full = self._buf(("full", par, gi), (s.world_size * s.block, b - a), X0)
-                new_works.append(self._all_gather(full, loc))
+                ev_l, ev_h = self._compute(src[gi], loc[:s.rows, :src[gi].shape[1]], layout,
+                                           split, key=(h, gi))
+                full = self._buf(("full", par, gi), (PB, b - a), X0)
+                if split:
+                    comm = self._streams[1]
+                    comm.wait_event(ev_l)
+                    comm.wait_event(ev_h)
+                    with torch.cuda.stream(comm):
+                        new_works.append(self._all_gather(full, loc))
+                else:
+                    new_works.append(self._all_gather(full, loc))
                 gathered.append(full)
-            works, src = new_works, gathered
+            works, src, layout = new_works, gathered, "gathered"
         if output == "sharded":
             # last hop: each group straight into this rank's rows of X_K
+            hub_events = []
             for gi, (a, b) in enumerate(groups):
                 if works[gi] is not None:
                     works[gi].wait()
                 bb = min(b, F)
-                if bb > a and s.rows:
-                    self.spmm_fn(s, src[gi][:, :bb - a], out[:, a:bb])
+                if bb > a:
+                    _, ev_h = self._compute(src[gi][:, :bb - a], out[:, a:bb], layout, split,
+                                            key=("last", gi))
+                    if ev_h is not None:
+                        hub_events.append(ev_h)
+            if hub_events:
+                main = torch.cuda.current_stream(X0.device)
+                for ev in hub_events:
+                    main.wait_event(ev)
             return out
         for w in works:
             if w is not None:
                 w.wait()
         if out is None:
             out = torch.empty((n, F), dtype=torch.float32, device=X0.device)
+        # compact the gathered blocks (row p*B + i -> global row bounds[p] + i)
         for gi, (a, b) in enumerate(groups):
             bb = min(b, F)
-            if bb > a:
+            if bb <= a:
+                continue
+            if s.identity_layout:  # block p already sits at rows [p*B, ...)
                 out[:, a:bb].copy_(src[gi][:n, :bb - a])
+                continue
+            for p in range(s.world_size):
+                r0, r1 = int(s.bounds[p]), int(s.bounds[p + 1])
+                if r1 > r0:
+                    out[r0:r1, a:bb].copy_(src[gi][p * s.block:p * s.block + (r1 - r0), :bb - a])
+        return out
+
+
+# ---------------------------------------------------------------------------
+# 2-D partition: row blocks x feature blocks.
+
+class TiledPropagator:
+    """X_K = S^K X_0 over P = R x C ranks: rank p = i*C + j owns row block i
+    (nnz-balanced over R) of feature block j (C equal,
+    4-aligned column blocks).  Each column block is an independent row
+    partition over its R ranks (RowPartitionedPropagator on the sub-group of
+    ranks holding block j): the all-gather between hops moves N x F/C floats
+    per rank instead of N x F, and each rank's launches cover N/R rows
+    instead of N/P, so every X line it gathers is reused by R/P-times more
+    rows than under a pure row partition.  The row partition is C = 1.
+    Bit-exact: each element is still one FMA chain over its row in CSR order.
+
+    output="sharded": this rank's full-width row block [rows_i, F], assembled
+    by one all-gather of the C tiles within the row group (ranks holding
+    block i); output="tile": just the [rows_i, F/C] tile.
+
+    Every rank must construct it collectively (it creates the sub-groups)."""
+
+    def __init__(self, row_ptr, col_idx, val, rank, world_size, col_blocks, device,
+                 group_floats=128, host_staging=False, balance="nnz", spmm_fn=None):
+        C = int(col_blocks)
+        if C < 1 or world_size % C:
+            raise ValueError(f"col_blocks={C} must divide world_size={world_size}")
+        R = world_size // C
+        self.R, self.C = R, C
+        self.i, self.j = rank // C, rank % C
+        self.rank, self.world_size = rank, world_size
+        self.host_staging = host_staging
+        # every rank creates every sub-group, in the same order
+        col_groups = [dist.new_group([i * C + j for i in range(R)]) for j in range(C)]
+        row_groups = [dist.new_group([i * C + j for j in range(C)]) for i in range(R)]
+        self.col_group, self.row_group = col_groups[self.j], row_groups[self.i]
+        self.shard = make_shard(row_ptr, col_idx, val, self.i, R, device, balance=balance)
+        self.prop = RowPartitionedPropagator(self.shard, group=self.col_group, spmm_fn=spmm_fn,
+                                             group_floats=group_floats,
+                                             host_staging=host_staging)
+        self._bufs = {}
+
+    @property
+    def row_begin(self):
+        return self.shard.row_begin
+
+    @property
+    def row_end(self):
+        return self.shard.row_end
+
+    def _buf(self, key, shape, like):
+        b = self._bufs.get(key)
+        if b is None or tuple(b.shape) != tuple(shape) or b.device != like.device:
+            b = torch.empty(shape, dtype=torch.float32, device=like.device)
+            self._bufs[key] = b
+        return b
+
+    def propagate(self, X0, K, out=None, output="sharded"):
+        if output not in ("sharded", "tile"):
+            raise ValueError(f"TiledPropagator output must be 'sharded' or 'tile', not {output!r}")
+        n, F = X0.shape
+        fb, Bf = feature_bounds(F, self.C)
+        c0, c1 = int(fb[self.j]), int(fb[self.j + 1])
+        rows = self.shard.rows
+        if K <= 0:
+            blk = X0[self.row_begin:self.row_end]
+            return blk if output == "sharded" else blk[:, c0:c1]
+        if self.C == 1:
+            return self.prop.propagate(X0, K, out=out, output="sharded")
+        tile = self._buf("tile", (max(1, rows), Bf), X0)[:rows]
+        if c1 > c0:
+            self.prop.propagate(X0[:, c0:c1], K, out=tile[:, :c1 - c0], output="sharded")
+        if output == "tile":
+            return tile[:, :c1 - c0]
+        full = self._buf("tiles", (self.C * max(1, rows), Bf), X0)
+        if self.host_staging:
+            h = torch.empty(full.shape, dtype=full.dtype)
+            dist.all_gather_into_tensor(h, self._buf("tile", (max(1, rows), Bf), X0).cpu(),
+                                        group=self.row_group)
+            full.copy_(h)
+        else:
+            dist.all_gather_into_tensor(full, self._buf("tile", (max(1, rows), Bf), X0),
+                                        group=self.row_group)
+        if out is None:
+            out = torch.empty((rows, F), dtype=torch.float32, device=X0.device)
+        R1 = max(1, rows)
+        for q in range(self.C):
+            q0, q1 = int(fb[q]), int(fb[q + 1])
+            if q1 > q0 and rows:
+                _copy_cols(full[q * R1:q * R1 + rows, :q1 - q0], out[:, q0:q1])
         return out
 
 

@@ -57,6 +57,8 @@ NO_PLAN = Plan(None, 0, 0, 0)
 
 SPMM_X_PADDED = 1  # sgc_spmm_csr_f32_ex flags (include/sgc_amd.h)
 SPMM_Y_PADDED = 2
+SPMM_NO_HUB = 4    # split launch: every row but the plan's hub rows
+SPMM_HUB_ONLY = 8  # split launch: only the hub rows, on the current stream
 
 STATUS_ROWS_SORTED = 1
 STATUS_COLS_ASCENDING = 2
@@ -297,8 +299,11 @@ def _check_features(X, csr):
 
 
 def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
-         use_plan=True, threshold=None, hub_threshold=None):
-    """One hop Y = S[row_begin:row_end] . X (bit-exact with torch.spmm on CPU)."""
+         use_plan=True, threshold=None, hub_threshold=None, flags=0):
+    """One hop Y = S[row_begin:row_end] . X (bit-exact with torch.spmm on CPU).
+    flags: SPMM_* bits of sgc_spmm_csr_f32_ex (a split launch on the GPU: NO_HUB
+    / HUB_ONLY; on the CPU the whole hop runs for the NO_HUB part and nothing
+    for HUB_ONLY, so the two parts still write every row once)."""
     X = _check_features(X, csr)
     row_end = csr.n_rows if row_end is None else row_end
     F = X.shape[1]
@@ -308,6 +313,8 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
         return out
     lib = _lib.load()
     if X.device.type == "cpu":
+        if flags & SPMM_HUB_ONLY:
+            return out
         _lib.check(lib.sgc_spmm_csr_f32_cpu(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
                                             _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
                                             X.stride(0), _lib.ptr(out), out.stride(0), F,
@@ -315,12 +322,44 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
         return out
     pl = csr.plan(row_begin, row_end, threshold, hub_threshold, F) if use_plan else NO_PLAN
     with torch.cuda.device(X.device):
-        _lib.check(lib.sgc_spmm_csr_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
-                                        _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
-                                        X.stride(0), _lib.ptr(out), out.stride(0), F,
-                                        _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
-                                        _lib.stream_handle(X.device)), "spmm_csr_f32")
+        _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
+                                           _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
+                                           X.stride(0), _lib.ptr(out), out.stride(0), F,
+                                           _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
+                                           int(flags), _lib.stream_handle(X.device)),
+                   "spmm_csr_f32")
     return out
+
+
+class SpmmLaunch:
+    """One prepared SpMM launch (fixed CSR, plan, X, out, flags): the ctypes
+    arguments are built once and each call only passes the stream.  The
+    multi-GPU pipeline replays a dozen launches per step, where the checks
+    and lookups of spmm() would cost more host time than the launches take on
+    the GPU.  The tensors must stay alive and unchanged in shape/storage."""
+
+    __slots__ = ("_fn", "_args", "_keep")
+
+    def __init__(self, csr: DeviceCSR, X: torch.Tensor, out: torch.Tensor, row_begin=0,
+                 row_end=None, flags=0, threshold=None, hub_threshold=None):
+        X = _check_features(X, csr)
+        if X.device.type != "cuda":
+            raise RuntimeError("SpmmLaunch: ROCm tensors only")
+        row_end = csr.n_rows if row_end is None else row_end
+        F = X.shape[1]
+        pl = csr.plan(row_begin, row_end, threshold, hub_threshold, F)
+        lib = _lib.load()
+        self._fn = lib.sgc_spmm_csr_f32_ex
+        self._keep = (csr, X, out, pl)
+        self._args = (_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val),
+                      int(row_begin), int(row_end), _lib.ptr(X), X.stride(0), _lib.ptr(out),
+                      out.stride(0), F, _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
+                      int(flags))
+
+    def __call__(self, stream_handle):
+        rc = self._fn(*self._args, stream_handle)
+        if rc:
+            _lib.check(rc, "spmm_csr_f32 (prepared)")
 
 
 def aligned_ld(F):

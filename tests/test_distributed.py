@@ -43,25 +43,27 @@ def test_equal_row_bounds():
     assert equal_row_bounds(8, 2).tolist() == [0, 4, 8]
 
 
-def _oracle_spmm(shard, X, out):
+def _oracle_spmm(shard, X, out, layout="input", part="all"):
     from oracle import oracle as o
     rp = shard.row_ptr.numpy()
-    Y = o.spmm_csr(rp, shard.col_idx.numpy(), shard.val.numpy(), X.numpy())
+    cols = shard.col_idx if layout == "input" else shard.col_gathered
+    Y = o.spmm_csr(rp, cols.numpy(), shard.val.numpy(), X.numpy())
     out.copy_(torch.from_numpy(Y))
     return out
 
 
 def _worker(rank, world, port, case, K, result_q, group_floats=128, staging=False,
-            output="replicated", autotune=False):
+            output="replicated", autotune=False, balance="nnz", engine="oracle"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from oracle import oracle as o
         n = int(case["n"])
         rp, ci, va = o.coo_to_csr(n, n, case["rows"], case["cols"], case["vals"])
-        shard = make_shard(rp, ci, va, rank, world, "cpu")
-        prop = RowPartitionedPropagator(shard, spmm_fn=_oracle_spmm, group_floats=group_floats,
-                                        host_staging=staging)
+        shard = make_shard(rp, ci, va, rank, world, "cpu", balance=balance)
+        # engine "product": the default spmm_fn, i.e. the library's CPU twin
+        prop = RowPartitionedPropagator(shard, spmm_fn=_oracle_spmm if engine == "oracle" else None,
+                                        group_floats=group_floats, host_staging=staging)
         X0 = torch.from_numpy(case["X"])
         tuned = None
         if autotune:
@@ -69,32 +71,40 @@ def _worker(rank, world, port, case, K, result_q, group_floats=128, staging=Fals
             assert sorted(times) == [8, 16, 64] and prop.group_floats in times
             tuned = prop.group_floats
         out = prop.propagate(X0, K, output=output)
-        result_q.put((rank, out.numpy()) if not autotune else (rank, (out.numpy(), tuned)))
+        res = (out.numpy(), shard.bounds)
+        result_q.put((rank, res) if not autotune else (rank, (res, tuned)))
     finally:
         dist.destroy_process_group()
 
 
 def _check_results(results, case, K, world, output, name):
     want = case[f"Y{K}"]
-    rb = equal_row_bounds(want.shape[0], world)
     for r in range(world):
+        got, rb = results[r]
         w = want if output == "replicated" else want[rb[r]:rb[r + 1]]
-        assert results[r].shape == w.shape, (name, r)
-        assert np.array_equal(results[r].view(np.uint32), w.view(np.uint32)), (name, r)
+        assert got.shape == w.shape, (name, r)
+        assert np.array_equal(got.view(np.uint32), w.view(np.uint32)), (name, r)
 
 
-@pytest.mark.parametrize("world,name,K,gf,staging,output", [
-    (2, "norm_n48_F65", 2, 128, False, "replicated"), (2, "hub1000_F65", 2, 16, False, "sharded"),
-    (3, "norm_n48_F602", 3, 128, False, "replicated"), (3, "norm_n48_F602", 2, 128, False, "sharded"),
-    (4, "raw_unsorted_dups_F7", 3, 2, False, "replicated"),
-    (4, "raw_unsorted_dups_F7", 1, 2, False, "sharded"),
-    (2, "isolated_F17", 1, 4, True, "replicated"), (2, "norm_n48_F130", 2, 64, True, "sharded")])
-def test_row_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, gf, staging, output):
+@pytest.mark.parametrize("world,name,K,gf,staging,output,balance,engine", [
+    (2, "norm_n48_F65", 2, 128, False, "replicated", "nnz", "oracle"),
+    (2, "hub1000_F65", 2, 16, False, "sharded", "nnz", "oracle"),
+    (3, "norm_n48_F602", 3, 128, False, "replicated", "rows", "oracle"),
+    (3, "norm_n48_F602", 2, 128, False, "sharded", "nnz", "product"),
+    (4, "raw_unsorted_dups_F7", 3, 2, False, "replicated", "nnz", "product"),
+    (4, "raw_unsorted_dups_F7", 1, 2, False, "sharded", "rows", "oracle"),
+    (2, "isolated_F17", 1, 4, True, "replicated", "nnz", "oracle"),
+    (2, "norm_n48_F130", 2, 64, True, "sharded", "nnz", "product"),
+    (3, "hub1000_F130", 2, 64, False, "replicated", "nnz", "product"),
+    (4, "hub1000_F65", 2, 32, False, "sharded", "rows", "product")])
+def test_row_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, gf, staging, output,
+                                      balance, engine):
     case = tiny_cases[name]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, K, q, gf, staging, output))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, K, q, gf, staging, output,
+                                               False, balance, engine))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -124,6 +134,74 @@ def test_row_partition_autotune_gloo(tiny_cases, oracle, output):
         assert p.exitcode == 0
     assert len({got[r][1] for r in range(world)}) == 1
     _check_results({r: got[r][0] for r in range(world)}, case, K, world, output, "autotune")
+
+
+def _tiled_worker(rank, world, port, case, K, C, result_q, staging, engine):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as o
+        from sgc_amd.distributed import TiledPropagator
+        n = int(case["n"])
+        rp, ci, va = o.coo_to_csr(n, n, case["rows"], case["cols"], case["vals"])
+        tp = TiledPropagator(rp, ci, va, rank, world, C, "cpu", group_floats=8,
+                             host_staging=staging,
+                             spmm_fn=_oracle_spmm if engine == "oracle" else None)
+        X0 = torch.from_numpy(case["X"])
+        out = tp.propagate(X0, K, output="sharded")
+        out2 = tp.propagate(X0, K, output="sharded")  # buffers reused
+        assert torch.equal(out, out2)
+        result_q.put((rank, (out.numpy(), np.repeat(tp.shard.bounds, 1))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,C,name,K,staging,engine", [
+    (4, 2, "norm_n48_F602", 2, False, "product"), (2, 2, "norm_n48_F65", 3, False, "oracle"),
+    (4, 4, "hub1000_F65", 2, False, "product"), (4, 2, "raw_unsorted_dups_F7", 2, True, "oracle"),
+    (6, 3, "norm_n48_F130", 2, False, "product")])
+def test_tiled_partition_gloo_bit_exact(tiny_cases, oracle, world, C, name, K, staging, engine):
+    """2-D partition (row blocks x feature blocks): every rank's full-width
+    row block of X_K equals the reference's rows, bit for bit."""
+    case = tiny_cases[name]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tiled_worker, args=(r, world, port, case, K, C, q, staging,
+                                                     engine)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = case[f"Y{K}"]
+    R = world // C
+    for r in range(world):
+        arr, rb = got[r]
+        i = r // C
+        w = want[rb[i]:rb[i + 1]]
+        assert arr.shape == w.shape and np.array_equal(arr.view(np.uint32), w.view(np.uint32)), r
+    del R
+
+
+def test_gathered_layout():
+    """nnz-balanced blocks of unequal rows: node j sits at row p*B + (j - r_p)
+    of the gathered buffer; equal blocks are the identity."""
+    from sgc_amd.distributed import gathered_index
+    rp = np.array([0, 100, 101, 102, 103, 203, 204, 205, 305])
+    b = nnz_balanced_bounds(rp, 3)
+    B = int(np.max(np.diff(b)))
+    g = gathered_index(b, B, np.arange(8))
+    for p in range(3):
+        for j in range(b[p], b[p + 1]):
+            assert g[j] == p * B + j - b[p]
+    assert len(set(g.tolist())) == 8
+    eb = equal_row_bounds(10, 4)
+    assert np.array_equal(gathered_index(eb, 3, np.arange(10)), np.arange(10))
+    sh = make_shard(np.arange(11), np.arange(10), np.ones(10, np.float32), 1, 4, "cpu",
+                    balance="rows")
+    assert sh.identity_layout and sh.col_gathered is sh.col_idx
 
 
 # ---------------------------------------------------------------------------
@@ -162,7 +240,7 @@ def _feature_worker(rank, world, port, case, K, result_q, chunks, align, staging
         out = prop.propagate(torch.from_numpy(case["X"]), K, output=output)
         out2 = prop.propagate(torch.from_numpy(case["X"]), K, output=output)  # buffers reused
         assert torch.equal(out, out2)
-        result_q.put((rank, out.numpy()))
+        result_q.put((rank, (out.numpy(), equal_row_bounds(n, world))))
     finally:
         dist.destroy_process_group()
 
