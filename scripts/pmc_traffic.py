@@ -60,7 +60,8 @@ def workload(shape):
     import torch
 
     from sgc_amd import _lib, graphs
-    from sgc_amd.propagate import DeviceCSR, aligned_ld, propagate, spmm
+    from sgc_amd.propagate import (SPMM_X_PADDED, SPMM_Y_PADDED, DeviceCSR, aligned_ld,
+                                   propagate, spmm)
     dev = torch.device("cuda", 0)
     spec = graphs.SHAPES[shape]
     F, K = spec["features"], spec["hops"]
@@ -77,8 +78,8 @@ def workload(shape):
     cal = DeviceCSR.from_host_arrays(rp, ci, va, device=dev)
     Xc = torch.randn((N_CAL, LD), device=dev)[:, :F]
     Yc = torch.empty((N_CAL, LD), device=dev)[:, :F]
-    for _ in range(REPEATS):
-        spmm(cal, Xc, out=Yc, use_plan=False)
+    for _ in range(REPEATS):  # the padded-buffer flags select the kernel the hops use
+        spmm(cal, Xc, out=Yc, use_plan=False, flags=SPMM_X_PADDED | SPMM_Y_PADDED)
     torch.cuda.synchronize()
     del Xc, Yc, cal
     S = graphs.synthetic_graph(shape, seed=0)
@@ -135,7 +136,8 @@ def _per_dispatch(rows, counter):
 
 def _launches(d, K):
     """(calibration dispatch ids, [[main id, hub ids...] per shape launch])."""
-    ks = sorted(k for k, (nm, _) in d.items() if "spmm_csr_kernel" in nm)
+    ks = sorted(k for k, (nm, _) in d.items()
+                if "spmm_csr_kernel" in nm or "spmm_rows_kernel" in nm)
     hubs = sorted(k for k, (nm, _) in d.items() if "spmm_hub_kernel" in nm)
     cal, main = ks[:REPEATS], ks[REPEATS:REPEATS + REPEATS * K]
     prev = [cal[-1]] + main[:-1]
@@ -172,7 +174,7 @@ def summarize(out_dir, shape):
     alg = 4 * (n + 1) + 8 * nnz + 4 * F * nnz + 4 * F * n
     comp = 4 * (n + 1) + 8 * nnz + 8 * F * n
     rec = {
-        "workload": f"{shape}-shape propagate() K={K} ({n} rows, {nnz} nnz, F={F}; X_0 re-laid "
+        "workload": f"{shape}-shape propagate() K={K} ({n} rows, {nnz} nnz, F={F}; X_0 in 128-B rows "
                     f"to ld {LD}, intermediates ld {LD}, last hop into ld {F}), {REPEATS} times; "
                     f"one launch = one hop (spmm_csr_kernel + its spmm_hub_kernel dispatches)",
         "lib_sha256": meta["lib_sha256"], "tuning": meta["tuning"],
