@@ -9,11 +9,12 @@ synthetic Reddit-shape graph (232,965 nodes, 11,606,919 undirected edges,
 nnz(S) = 23,446,803, F = 602, K = 2), inputs resident in HBM.
 A "step" = one full K-hop propagation.  N > 1 (sgc_amd.distributed), total
 work fixed, so scaling is "strong":
-  --partition rows (default)  S row-partitioned (nnz-balanced row blocks,
-                SURVEY.md 8(e)); RCCL all-gather of X_k after each hop that feeds
-                another, pipelined in feature groups, hub rows on their own streams
+  --partition rows  S row-partitioned (nnz-balanced row blocks, SURVEY.md
+                8(e)); RCCL all-gather of X_k after each hop that feeds another,
+                optionally pipelined in feature groups, hub rows on their own streams
   --partition tiles  R x C: row blocks x --col-blocks feature blocks; the
                 per-hop all-gather runs within each feature block's R ranks
+  --partition auto (default)  rows vs tiles, timed on the node
   --partition features  each rank runs all K hops on its block of feature
                 columns over the full S, no exchange between hops
   --output sharded (default)  each rank ends with its row block of X_K
@@ -346,6 +347,7 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
     its compulsory bytes (its rows of S, the X columns it reads once, its Y)
     are recorded."""
     n, F = X0.shape
+    tp = None
 
     def bracket(fn, nbytes):
         def run(*a, **k):
@@ -394,7 +396,7 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
 
         C = args.col_blocks if args.partition == "tiles" else 1
         auto = args.group_floats == "auto"
-        gf0 = 128 if auto else int(args.group_floats)
+        gf0 = 0 if auto else int(args.group_floats)
         spmm_fn = bracket(_default_spmm, launch_bytes)
         if C > 1:
             if output != "sharded":
@@ -408,7 +410,7 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
             shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
             prop = RowPartitionedPropagator(shard, spmm_fn=spmm_fn, group_floats=gf0,
                                             host_staging=staging)
-            tp, Xa = None, X0
+            Xa = X0
         tuned = ""
         if auto and shard.world_size > 1:  # untimed setup, like the plans
             tt = prop.autotune(Xa, K, output="sharded" if C > 1 else output)
@@ -429,7 +431,7 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
     out = torch.empty((n, F), device=dev) if output == "replicated" else None
 
     def step():
-        if args.partition == "tiles" and tp is not None:
+        if tp is not None:
             return tp.propagate(X0, K, output="sharded")
         return prop.propagate(X0, K, out=out, output=output)
     return step, par, unit
@@ -451,14 +453,16 @@ def main():
     ap.add_argument("--hub-threshold", type=int, default=None, help="hub-row threshold")
     ap.add_argument("--group-floats", default="auto",
                     help="N>1 rows: feature-group width of the compute/all-gather pipeline "
-                         "(an integer, or auto = timed on this node among 128/256/224)")
+                         "(an integer, 0 = one full-width group, or auto = timed on this node "
+                         "among 0/256/128)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo = host-staged rehearsal of the N>1 path (ranks may share a GPU)")
     ap.add_argument("--distributed-path", action="store_true",
                     help="run the N>1 path even at N=1 (exercises RCCL on one GPU)")
-    ap.add_argument("--partition", default="rows", choices=["rows", "tiles", "features"],
+    ap.add_argument("--partition", default="auto", choices=["auto", "rows", "tiles", "features"],
                     help="N>1: split the rows of S (per-hop all-gather), rows x feature blocks "
-                         "(tiles, --col-blocks), or the feature columns")
+                         "(tiles, --col-blocks), the feature columns, or auto = rows vs tiles "
+                         "timed on the node")
     ap.add_argument("--col-blocks", type=int, default=2,
                     help="N>1 tiles: feature blocks C (P = R x C)")
     ap.add_argument("--output", default="sharded", choices=["sharded", "replicated"],
@@ -538,14 +542,34 @@ def main():
     n, F, nnz = S.n, X_host.shape[1], S.nnz
     X0 = torch.from_numpy(X_host).to(dev)
     tm = {"on": False, "pairs": [], "bytes": []}
-    step, parallelism, unit_desc = build_dist_step(args, S, X0, dev, rank, world, K, args.output,
-                                                   tm)
+    if args.partition == "auto":
+        # row partition vs 2-D tiles: timed on this node (max over ranks), so
+        # the exchange rate the node actually has decides, not an estimate
+        import copy
+        cands = ["rows"]
+        if world >= 4 and world % args.col_blocks == 0 and args.output == "sharded":
+            cands.append("tiles")
+        trials = {}
+        for cand in cands:
+            a = copy.copy(args)
+            a.partition = cand
+            t_c = {"on": False, "pairs": [], "bytes": []}
+            built = build_dist_step(a, S, X0, dev, rank, world, K, args.output, t_c)
+            e_c, _, _ = timed(built[0], 3, 1, True, dev)
+            trials[cand] = (e_c / 3, built, t_c)
+        best = min(trials, key=lambda c: (trials[c][0], c))
+        _, (step, parallelism, unit_desc), tm = trials[best]
+        parallelism += " [auto-selected: " + ", ".join(
+            f"{c} {trials[c][0] * 1e3:.2f} ms" for c in cands) + "]"
+    else:
+        step, parallelism, unit_desc = build_dist_step(args, S, X0, dev, rank, world, K,
+                                                       args.output, tm)
     elapsed, step_ms, _ = timed(step, args.steps, args.warmup, True, dev,
                                 on_start=lambda: tm.update(on=True),
                                 on_stop=lambda: tm.update(on=False))
     launch_ms = [s.elapsed_time(e) for s, e in tm["pairs"]]
     alt = None
-    if args.alt_steps > 0 and args.partition != "tiles":
+    if args.alt_steps > 0 and "tiles" not in parallelism:
         alt_mode = "replicated" if args.output == "sharded" else "sharded"
         alt_step, alt_par, _ = build_dist_step(args, S, X0, dev, rank, world, K, alt_mode,
                                                {"on": False})

@@ -110,6 +110,10 @@ def main():
     ap.add_argument("--group-floats", type=int, default=128)
     ap.add_argument("--bw", default="300,450,600", help="assumed all-gather ingress GB/s per rank")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--row-chunks", type=int, default=1,
+                    help="exchanged hops in this many full-width row chunks (group floats 0)")
+    ap.add_argument("--no-split", action="store_true",
+                    help="hub rows inside each group launch (side stream, joined per launch)")
     args = ap.parse_args()
     spec = graphs.SHAPES[args.shape]
     S = graphs.synthetic_graph(args.shape, seed=0)
@@ -137,7 +141,9 @@ def main():
             for j in range(C):
                 c0, c1 = int(fb[j]), int(fb[j + 1])
                 Xj = X0[:, c0:c1]
-                prop = LocalRowPropagator(shard, group_floats=args.group_floats)
+                prop = LocalRowPropagator(shard, group_floats=args.group_floats,
+                                          split_hubs=not args.no_split,
+                                          row_chunks=args.row_chunks)
                 t = timeit(lambda: prop.propagate(Xj, K, output="sharded"), args.reps)
                 h0 = time.perf_counter()
                 for _ in range(3):

@@ -154,9 +154,12 @@ int coo_to_csr_cpu(const int64_t *rows, const int64_t *cols, const float *vals, 
 int spmm_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val, int64_t row_begin,
              int64_t row_end, const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
              int32_t n_threads) {
-    SGC_REQUIRE(row_ptr && col_idx && val && X && Y, SGC_EINVAL, "spmm_cpu: null pointer");
+    SGC_REQUIRE(row_ptr && X && Y, SGC_EINVAL, "spmm_cpu: null pointer");
     SGC_REQUIRE(row_begin >= 0 && row_end >= row_begin && row_end < INT32_MAX, SGC_ERANGE,
                 "spmm_cpu: bad row range [%lld, %lld)", (long long)row_begin, (long long)row_end);
+    // col_idx / val may be NULL only when the rows hold no nonzeros (an empty shard)
+    SGC_REQUIRE((col_idx && val) || row_ptr[row_end] == row_ptr[row_begin], SGC_EINVAL,
+                "spmm_cpu: null col_idx/val");
     SGC_REQUIRE(F >= 0 && ldx >= F && ldy >= F, SGC_EINVAL, "spmm_cpu: bad shape");
     const int64_t n = row_end - row_begin;
     if (n == 0 || F == 0) return SGC_OK;

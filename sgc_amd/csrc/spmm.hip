@@ -1081,7 +1081,9 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
                 int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
                 int64_t ldy, int64_t F, const int32_t *heavy_rows, int64_t n_heavy,
                 int64_t n_hub, int32_t heavy_threshold, uint32_t flags, hipStream_t stream) {
-    SGC_REQUIRE(row_ptr && col_idx && val && X && Y, SGC_EINVAL, "spmm: null pointer");
+    // col_idx / val may be NULL for a CSR without nonzeros (torch's empty
+    // tensors have no storage): the kernels never dereference them then
+    SGC_REQUIRE(row_ptr && X && Y, SGC_EINVAL, "spmm: null pointer");
     SGC_REQUIRE(row_begin >= 0 && row_end >= row_begin && row_end < INT32_MAX, SGC_ERANGE,
                 "spmm: bad row range [%lld, %lld)", (long long)row_begin, (long long)row_end);
     SGC_REQUIRE(F > 0 && F < (1 << 24), SGC_EINVAL, "spmm: bad feature count %lld", (long long)F);

@@ -113,6 +113,34 @@ class ShardCSR:
     def gathered_rows(self):
         return self.world_size * self.block
 
+    def cols_for(self, layout):
+        """Column ids of this rank's CSR for an input layout: "input" (global
+        node ids: the caller's X_0), "gathered" (the [P*B, F] exchange buffer)
+        or "gathered:RC" (the row-chunked exchange buffer, see
+        RowPartitionedPropagator(row_chunks=RC))."""
+        if layout == "input":
+            return self.col_idx
+        rc = int(layout.split(":")[1]) if ":" in layout else 1
+        if rc == 1:
+            return self.col_gathered
+        cache = self.__dict__.setdefault("_chunked_cols", {})
+        if rc not in cache:
+            Bc = -(-self.block // rc)
+            b = torch.as_tensor(self.bounds, dtype=torch.int64, device=self.col_idx.device)
+            j = self.col_idx.to(torch.int64)
+            q = torch.searchsorted(b, j, right=True) - 1
+            i = j - b[q]
+            pos = (i // Bc) * (self.world_size * Bc) + q * Bc + i % Bc
+            cache[rc] = pos.to(torch.int32)
+        return cache[rc]
+
+    def rows_for(self, layout):
+        """Rows of the buffer a layout names (its CSR's column count)."""
+        if layout == "input":
+            return self.n
+        rc = int(layout.split(":")[1]) if ":" in layout else 1
+        return rc * self.world_size * (-(-self.block // rc))
+
     @property
     def identity_layout(self):
         """Global row j sits at row j of the gathered buffer (equal blocks)."""
@@ -141,7 +169,7 @@ def make_shard(row_ptr, col_idx, val, rank, world_size, device, balance="nnz"):
                     t(np.asarray(val[k0:k1]), torch.float32), int(row_ptr.shape[0] - 1), cg)
 
 
-def _default_spmm(shard: ShardCSR, X, out, layout="input", part="all"):
+def _default_spmm(shard: ShardCSR, X, out, layout="input", part="all", rows=None):
     """This rank's rows of S.X through the product engine (HIP on ROCm
     tensors, the CPU twin on CPU tensors).  layout: "input" = X is the
     caller's [N, F] X_0 (global column ids), "gathered" = X is the [P*B, F]
@@ -155,21 +183,21 @@ def _default_spmm(shard: ShardCSR, X, out, layout="input", part="all"):
     cache = shard.__dict__.setdefault("_csr_by_layout", {})
     csr = cache.get(layout)
     if csr is None:
-        cols = shard.col_idx if layout == "input" else shard.col_gathered
-        n_cols = shard.n if layout == "input" else shard.gathered_rows
-        csr = DeviceCSR(shard.rows, n_cols, shard.row_ptr, cols, shard.val)
+        csr = DeviceCSR(shard.rows, shard.rows_for(layout), shard.row_ptr,
+                        shard.cols_for(layout), shard.val)
         cache[layout] = csr
     flags = {"all": 0, "light": SPMM_NO_HUB, "hub": SPMM_HUB_ONLY}[part]
+    r0, r1 = rows if rows is not None else (0, shard.rows)
     if not X.is_cuda:
-        return spmm(csr, X, 0, shard.rows, out=out, flags=flags)
+        return spmm(csr, X, r0, r1, out=out, flags=flags)
     launches = shard.__dict__.setdefault("_launches", {})
-    key = (layout, part, X.data_ptr(), tuple(X.shape), X.stride(0), out.data_ptr(),
+    key = (layout, part, r0, r1, X.data_ptr(), tuple(X.shape), X.stride(0), out.data_ptr(),
            tuple(out.shape), out.stride(0))
     fn = launches.get(key)
     if fn is None:
         if len(launches) > 256:
             launches.clear()
-        fn = launches[key] = SpmmLaunch(csr, X, out, 0, shard.rows, flags)
+        fn = launches[key] = SpmmLaunch(csr, X, out, r0, r1, flags)
     fn(_lib.stream_handle(X.device))
     return out
 
@@ -196,8 +224,9 @@ class RowPartitionedPropagator:
     default is the product engine (tests inject the CPU oracle)."""
 
     def __init__(self, shard: ShardCSR, group=None, spmm_fn: Optional[Callable] = None,
-                 group_floats: int = 128, host_staging: bool = False,
-                 pad_input: Optional[bool] = None, split_hubs: bool = True):
+                 group_floats: int = 0, host_staging: bool = False,
+                 pad_input: Optional[bool] = None, split_hubs: bool = True,
+                 row_chunks: int = 1):
         self.shard = shard
         # Re-lay X_0 into 128-B rows before hop 1?  The copy (all N rows, ~0.2 ms
         # at Reddit shape) beats reading 8-B aligned rows only while this rank's
@@ -206,10 +235,15 @@ class RowPartitionedPropagator:
         self.pad_input = pad_input
         self.group = group
         self.spmm_fn = spmm_fn or _default_spmm
-        self.group_floats = max(2, int(group_floats) // 2 * 2)  # 8-B aligned groups
+        # 0 = one group (full-width launches, no compute/exchange overlap);
+        # else 8-B aligned groups of this many floats
+        self.group_floats = 0 if int(group_floats) <= 0 else max(2, int(group_floats) // 2 * 2)
         # rehearsal only: gather device buffers through host copies (gloo)
         self.host_staging = host_staging
         self.split_hubs = split_hubs
+        # > 1: exchanged hops run full width in this many row chunks, each
+        # all-gathered as soon as it is done (one feature group)
+        self.row_chunks = max(1, int(row_chunks))
         self._bufs = {}
         self._streams = None
         self._hub_streams = []
@@ -233,14 +267,16 @@ class RowPartitionedPropagator:
         full.copy_(h_full)
         return None
 
-    def autotune(self, X0, K, output="sharded", candidates=(128, 256, 224), reps=2):
+    def autotune(self, X0, K, output="sharded", candidates=(0, "r4", 256, 128), reps=2):
         """Pick group_floats by timing whole propagations (collective: every
         rank must call it with the same arguments).  The best grouping depends
-        on the exchange rate, which only the node knows: with a fast all-gather
-        the hop after it is compute-bound and fewer, wider groups (cheaper
-        launches) win; with a slow one more groups hide more of it
-        (DESIGN.md 6).  Each candidate's time is the max over ranks, so every
-        rank picks the same width (the all-gathers' shapes must agree).
+        on the exchange rate, which only the node knows: narrower groups hide
+        more of the all-gather behind compute but each group launch re-reads
+        the CSR and pays a launch tail -- on one GPU a rank's P=8 step takes
+        1.7 ms as one full-width group (0) and 2.3-2.9 ms in 128-float groups
+        (profiles/r02/p8_rehearsal_*.log), so only a slow exchange favours
+        groups.  Each candidate's time is the max over ranks, so every rank
+        picks the same width (the all-gathers' shapes must agree).
         Returns {group_floats: seconds per propagation}."""
         import time
 
@@ -252,7 +288,13 @@ class RowPartitionedPropagator:
         on_dev = X0.is_cuda and dist.get_backend(self.group) == "nccl"
         times = {}
         for gf in candidates:
-            self.group_floats = max(2, int(gf) // 2 * 2)
+            # an int = feature-group width (0: one group); "rN" = one group in
+            # N row chunks per exchanged hop
+            if isinstance(gf, str) and gf.startswith("r"):
+                self.group_floats, self.row_chunks = 0, int(gf[1:])
+            else:
+                self.group_floats = 0 if int(gf) <= 0 else max(2, int(gf) // 2 * 2)
+                self.row_chunks = 1
             self._bufs.clear()
             self.propagate(X0, K, output=output)  # warm-up: buffers, plans
             sync()
@@ -263,31 +305,107 @@ class RowPartitionedPropagator:
             t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64,
                              device=X0.device if on_dev else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-            times[self.group_floats] = float(t.item())
-        self.group_floats = min(times, key=lambda g: (times[g], g))
+            times[gf] = float(t.item())
+        best = min(times, key=lambda g: (times[g], str(g)))
+        if isinstance(best, str):
+            self.group_floats, self.row_chunks = 0, int(best[1:])
+        else:
+            self.group_floats = 0 if int(best) <= 0 else max(2, int(best) // 2 * 2)
+            self.row_chunks = 1
         self._bufs.clear()
         return times
 
-    def _compute(self, X, out, layout, split, key=None):
-        """One group's local SpMM: (light event, hub event) on the GPU when the
-        launch is split, else (None, None) after one launch."""
+    def _compute(self, X, out, layout, split, key=None, rows=None):
+        """One group's (or row chunk's) local SpMM: (light event, hub event) on
+        the GPU when the launch is split, else (None, None) after one launch."""
+        kw = {} if rows is None else {"rows": rows}
+        n_rows = self.shard.rows if rows is None else rows[1] - rows[0]
         if not split:
-            if self.shard.rows:
-                self.spmm_fn(self.shard, X, out, layout, "all")
+            if n_rows:
+                self.spmm_fn(self.shard, X, out, layout, "all", **kw)
             return None, None
         main = torch.cuda.current_stream(X.device)
         hub_s = self._hub_stream(key[1], X.device)
         ready, ev_l, ev_h = self._events(key)
         ready.record(main)
-        if self.shard.rows:
-            self.spmm_fn(self.shard, X, out, layout, "light")
+        if n_rows:
+            self.spmm_fn(self.shard, X, out, layout, "light", **kw)
         ev_l.record(main)
         hub_s.wait_event(ready)
         with torch.cuda.stream(hub_s):
-            if self.shard.rows:
-                self.spmm_fn(self.shard, X, out, layout, "hub")
+            if n_rows:
+                self.spmm_fn(self.shard, X, out, layout, "hub", **kw)
         ev_h.record(hub_s)
         return ev_l, ev_h
+
+    def _issue_gather(self, full, loc, ev_l, ev_h, split):
+        if split:
+            comm = self._streams[1]
+            comm.wait_event(ev_l)
+            comm.wait_event(ev_h)
+            with torch.cuda.stream(comm):
+                return self._all_gather(full, loc)
+        return self._all_gather(full, loc)
+
+    def _propagate_row_chunks(self, X0, K, out, output, F, Fp, split):
+        """Exchanged hops at full width in RC row chunks: chunk c of every rank
+        is all-gathered into rows [c*P*Bc, (c+1)*P*Bc) of the exchange buffer
+        as soon as it is computed, so the hop's exchange overlaps its own
+        later chunks (the next hop needs all of X_k: every row reads every
+        column block, in column order).  Layout "gathered:RC" remaps the
+        columns (ShardCSR.cols_for).  X0 is the caller's [N, F] or its
+        128-B-row copy [N, Fp]; exchanged buffers are [., Fp] (pad columns
+        carry don't-care values and are never returned)."""
+        s = self.shard
+        n = X0.shape[0]
+        RC = self.row_chunks
+        Bc = -(-s.block // RC)
+        PB = RC * s.world_size * Bc
+        src, layout, works = X0, "input", []
+        K_ex = K - 1 if output == "sharded" else K
+        for h in range(K_ex):
+            for w in works:
+                if w is not None:
+                    w.wait()  # all of X_h has arrived
+            W = min(src.shape[1], Fp)
+            full = self._buf(("cfull", h & 1), (PB, Fp), X0)
+            works = []
+            for c in range(RC):
+                lo, hi = c * Bc, min((c + 1) * Bc, s.rows)
+                loc = self._buf(("cloc", h & 1, c), (Bc, Fp), X0)
+                ev_l = ev_h = None
+                if hi > lo:
+                    ev_l, ev_h = self._compute(src[:, :W], loc[:hi - lo, :W], layout, split,
+                                               key=("chunk", h, c), rows=(lo, hi))
+                elif split:
+                    _, ev_l, ev_h = self._events(("chunk", h, c))
+                    main = torch.cuda.current_stream(X0.device)
+                    ev_l.record(main)
+                    ev_h.record(main)
+                seg = full[c * s.world_size * Bc:(c + 1) * s.world_size * Bc]
+                works.append(self._issue_gather(seg, loc, ev_l, ev_h, split))
+            src, layout = full, f"gathered:{RC}"
+        for w in works:
+            if w is not None:
+                w.wait()
+        if output == "sharded":
+            if out is None:
+                out = torch.empty((s.rows, F), dtype=torch.float32, device=X0.device)
+            if s.rows:
+                _, ev_h = self._compute(src[:, :F], out, layout, split, key=("chunk", "last"))
+                if ev_h is not None:
+                    torch.cuda.current_stream(X0.device).wait_event(ev_h)
+            return out
+        if out is None:
+            out = torch.empty((n, F), dtype=torch.float32, device=X0.device)
+        for q in range(s.world_size):
+            r0, r1 = int(s.bounds[q]), int(s.bounds[q + 1])
+            for c in range(RC):
+                a, b = r0 + c * Bc, min(r0 + (c + 1) * Bc, r1)
+                if b > a:
+                    base = c * s.world_size * Bc + q * Bc
+                    out[a:b].copy_(src[base:base + (b - a), :F])
+        return out
 
     def _hub_stream(self, gi, device):
         """One stream per feature group for its hub rows: the hub kernels of a
@@ -336,9 +454,11 @@ class RowPartitionedPropagator:
                     _lib.ptr(X0), X0.stride(0), _lib.ptr(Xa), Fp, n, F,
                     _lib.stream_handle(X0.device)), "pad_rows_f32")
                 X0 = Xa
+        if self.row_chunks > 1 and s.world_size > 1:
+            return self._propagate_row_chunks(X0, K, out, output, F, Fp, split)
         # one group on a single rank: nothing to overlap, and each extra group
         # re-reads the CSR and adds a launch tail (+35% at world 1, r01)
-        gf = self.group_floats if s.world_size > 1 else Fp
+        gf = self.group_floats if s.world_size > 1 and self.group_floats > 0 else Fp
         groups = [(a, min(Fp, a + gf)) for a in range(0, Fp, gf)]
         src = [X0[:, a:min(b, X0.shape[1])] for a, b in groups]  # unpadded: last one narrower
         layout = "input"
@@ -360,14 +480,7 @@ class RowPartitionedPropagator:
                 ev_l, ev_h = self._compute(src[gi], loc[:s.rows, :src[gi].shape[1]], layout,
                                            split, key=(h, gi))
                 full = self._buf(("full", par, gi), (PB, b - a), X0)
-                if split:
-                    comm = self._streams[1]
-                    comm.wait_event(ev_l)
-                    comm.wait_event(ev_h)
-                    with torch.cuda.stream(comm):
-                        new_works.append(self._all_gather(full, loc))
-                else:
-                    new_works.append(self._all_gather(full, loc))
+                new_works.append(self._issue_gather(full, loc, ev_l, ev_h, split))
                 gathered.append(full)
             works, src, layout = new_works, gathered, "gathered"
         if output == "sharded":
@@ -428,7 +541,7 @@ class TiledPropagator:
     Every rank must construct it collectively (it creates the sub-groups)."""
 
     def __init__(self, row_ptr, col_idx, val, rank, world_size, col_blocks, device,
-                 group_floats=128, host_staging=False, balance="nnz", spmm_fn=None):
+                 group_floats=0, host_staging=False, balance="nnz", spmm_fn=None):
         C = int(col_blocks)
         if C < 1 or world_size % C:
             raise ValueError(f"col_blocks={C} must divide world_size={world_size}")

@@ -43,17 +43,17 @@ def test_equal_row_bounds():
     assert equal_row_bounds(8, 2).tolist() == [0, 4, 8]
 
 
-def _oracle_spmm(shard, X, out, layout="input", part="all"):
+def _oracle_spmm(shard, X, out, layout="input", part="all", rows=None):
     from oracle import oracle as o
     rp = shard.row_ptr.numpy()
-    cols = shard.col_idx if layout == "input" else shard.col_gathered
-    Y = o.spmm_csr(rp, cols.numpy(), shard.val.numpy(), X.numpy())
+    r0, r1 = rows if rows is not None else (0, shard.rows)
+    Y = o.spmm_csr(rp, shard.cols_for(layout).numpy(), shard.val.numpy(), X.numpy(), r0, r1)
     out.copy_(torch.from_numpy(Y))
     return out
 
 
 def _worker(rank, world, port, case, K, result_q, group_floats=128, staging=False,
-            output="replicated", autotune=False, balance="nnz", engine="oracle"):
+            output="replicated", autotune=False, balance="nnz", engine="oracle", row_chunks=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -63,13 +63,14 @@ def _worker(rank, world, port, case, K, result_q, group_floats=128, staging=Fals
         shard = make_shard(rp, ci, va, rank, world, "cpu", balance=balance)
         # engine "product": the default spmm_fn, i.e. the library's CPU twin
         prop = RowPartitionedPropagator(shard, spmm_fn=_oracle_spmm if engine == "oracle" else None,
-                                        group_floats=group_floats, host_staging=staging)
+                                        group_floats=group_floats, host_staging=staging,
+                                        row_chunks=row_chunks)
         X0 = torch.from_numpy(case["X"])
         tuned = None
         if autotune:
-            times = prop.autotune(X0, K, output=output, candidates=(8, 64, 16), reps=1)
-            assert sorted(times) == [8, 16, 64] and prop.group_floats in times
-            tuned = prop.group_floats
+            times = prop.autotune(X0, K, output=output, candidates=(8, 64, 16, 0, "r3"), reps=1)
+            assert sorted(times, key=str) == sorted([8, 16, 64, 0, "r3"], key=str)
+            tuned = (prop.group_floats, prop.row_chunks)
         out = prop.propagate(X0, K, output=output)
         res = (out.numpy(), shard.bounds)
         result_q.put((rank, res) if not autotune else (rank, (res, tuned)))
@@ -96,15 +97,19 @@ def _check_results(results, case, K, world, output, name):
     (2, "isolated_F17", 1, 4, True, "replicated", "nnz", "oracle"),
     (2, "norm_n48_F130", 2, 64, True, "sharded", "nnz", "product"),
     (3, "hub1000_F130", 2, 64, False, "replicated", "nnz", "product"),
-    (4, "hub1000_F65", 2, 32, False, "sharded", "rows", "product")])
+    (4, "hub1000_F65", 2, 32, False, "sharded", "rows", "product"),
+    (3, "hub1000_F65", 2, 0, False, "replicated", "nnz", "product:rc4"),
+    (2, "norm_n48_F602", 2, 0, False, "sharded", "nnz", "oracle:rc3"),
+    (4, "raw_unsorted_dups_F7", 3, 0, True, "sharded", "rows", "product:rc2")])
 def test_row_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, gf, staging, output,
                                       balance, engine):
     case = tiny_cases[name]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
+    eng, _, rc = engine.partition(":rc")
     procs = [ctx.Process(target=_worker, args=(r, world, port, case, K, q, gf, staging, output,
-                                               False, balance, engine))
+                                               False, balance, eng, int(rc or 1)))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -319,6 +319,20 @@ def test_narrow_launches_rows_kernel(oracle, F):
         assert bits_equal(out.cpu().numpy(), want), (F, th, hub)
 
 
+def test_empty_csr_writes_zeros():
+    """A CSR without a single nonzero (an empty shard: torch's empty col/val
+    tensors have no storage) writes +0.0 rows, like torch.spmm."""
+    from sgc_amd.propagate import DeviceCSR, spmm
+    csr = DeviceCSR.from_host_arrays(np.zeros(6, np.int32), np.zeros(0, np.int32),
+                                     np.zeros(0, np.float32), n_cols=7)
+    X = torch.randn(7, 65, device=DEV)
+    out = torch.full((5, 65), float("nan"), device=DEV)
+    spmm(csr, X, out=out)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    assert np.array_equal(o.view(np.uint32), np.zeros_like(o).view(np.uint32))
+
+
 def test_fused_xent_rejects_bad_labels():
     from sgc_amd.propagate import linear_xent
     X = torch.randn(10, 8, device=DEV)
