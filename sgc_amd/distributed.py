@@ -325,7 +325,7 @@ class RowPartitionedPropagator:
                 self.spmm_fn(self.shard, X, out, layout, "all", **kw)
             return None, None
         main = torch.cuda.current_stream(X.device)
-        hub_s = self._hub_stream(key[1], X.device)
+        hub_s = self._hub_stream(key[-1] if isinstance(key[-1], int) else 0, X.device)
         ready, ev_l, ev_h = self._events(key)
         ready.record(main)
         if n_rows:
