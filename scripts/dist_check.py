@@ -1,0 +1,90 @@
+"""Bit-exactness of the N-rank paths at full BASELINE size, rehearsed on ONE GPU.
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
+        scripts/dist_check.py [--shape reddit] [--partition rows|tiles] [--col-blocks 2]
+
+Every rank drives the same GPU (cuda:0) with the gloo backend (host-staged
+all-gathers, so no RCCL peer access is needed), runs the exact product
+propagator of bench.py (nnz-balanced row blocks, split hub launches, the
+autotuned pipeline) and keeps its sharded rows of X_K; rank 0 collects every
+block and compares the SHA-256 of the assembled X_K with the reference's own
+golden (tests/golden/shapes.json).  One JSON line from rank 0.
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from sgc_amd import graphs  # noqa: E402
+from sgc_amd.distributed import RowPartitionedPropagator, TiledPropagator, make_shard  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="reddit")
+    ap.add_argument("--partition", default="rows", choices=["rows", "tiles"])
+    ap.add_argument("--col-blocks", type=int, default=2)
+    ap.add_argument("--row-chunks", type=int, default=1)
+    ap.add_argument("--group-floats", type=int, default=0)
+    ap.add_argument("--device", default="cuda", help="cpu: the CPU-twin rehearsal")
+    args = ap.parse_args()
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if args.device == "cuda":
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+    else:
+        dev = torch.device("cpu")
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "shapes.json")))[args.shape]
+    spec = graphs.SHAPES[args.shape]
+    t0 = time.time()
+    S = graphs.synthetic_graph(args.shape, seed=g["seed"])
+    X = torch.from_numpy(graphs.synthetic_features(args.shape, g["n"], g["features"],
+                                                   seed=g["feature_seed"])).to(dev)
+    K = spec["hops"]
+    if args.partition == "tiles":
+        tp = TiledPropagator(S.row_ptr, S.col_idx, S.val, rank, world, args.col_blocks, dev,
+                             group_floats=args.group_floats, host_staging=True)
+        tp.prop.row_chunks = args.row_chunks
+        mine = tp.propagate(X, K, output="sharded")
+        r0, r1 = tp.row_begin, tp.row_end
+    else:
+        shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
+        prop = RowPartitionedPropagator(shard, group_floats=args.group_floats, host_staging=True,
+                                        row_chunks=args.row_chunks)
+        mine = prop.propagate(X, K, output="sharded")
+        r0, r1 = shard.row_begin, shard.row_end
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    blocks = [None] * world
+    dist.all_gather_object(blocks, (r0, r1, mine.cpu().numpy()))
+    if rank == 0:
+        Y = np.empty((g["n"], g["features"]), np.float32)
+        covered = np.zeros(g["n"], bool)
+        for a, b, arr in blocks:
+            if b > a and not covered[a:b].any():  # tiles: C ranks share a row block
+                Y[a:b] = arr
+                covered[a:b] = True
+        ok = bool(covered.all()) and hashlib.sha256(Y.tobytes()).hexdigest() == \
+            g["outputs"][str(K)]["sha"]
+        print(json.dumps({"shape": args.shape, "world": world, "partition": args.partition,
+                          "col_blocks": args.col_blocks if args.partition == "tiles" else 1,
+                          "row_chunks": args.row_chunks, "group_floats": args.group_floats,
+                          "rows_per_rank": [int(b - a) for a, b, _ in blocks],
+                          "bit_exact_vs_reference_hash": ok,
+                          "seconds": round(time.time() - t0, 1)}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

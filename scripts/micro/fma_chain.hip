@@ -475,6 +475,340 @@ __global__ void ring_X12(float *out, long long *cyc, int iters, float vc) {
     if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 
+
+__global__ void ring_B64x8(float *out, long long *cyc, int iters, float vc) {
+    __shared__ __attribute__((aligned(16))) float x[64 * 260];
+    __shared__ __attribute__((aligned(16))) float v[512];
+    for (int i = threadIdx.x; i < 64 * 260; i += blockDim.x) x[i] = 1e-3f * (i % 97);
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) v[i] = 0.5f + 1e-3f * i;
+    __syncthreads();
+    typedef __attribute__((address_space(3))) const float lds_f;
+    uint32_t xa = (uint32_t)(size_t)(lds_f *)(&x[threadIdx.x * 260]);
+    uint32_t va = (uint32_t)(size_t)(lds_f *)(&v[0]);
+    float acc = 0;
+    int it = iters;
+    long long t0 = __builtin_amdgcn_s_memtime();
+    asm volatile(
+            "s_waitcnt lgkmcnt(0)\n"
+            "ds_read_b64 v[80:81], %[xa] offset:0\n"
+            "ds_read_b64 v[82:83], %[xa] offset:8\n"
+            "ds_read_b64 v[84:85], %[xa] offset:16\n"
+            "ds_read_b64 v[86:87], %[xa] offset:24\n"
+            "ds_read_b64 v[88:89], %[xa] offset:32\n"
+            "ds_read_b64 v[90:91], %[xa] offset:40\n"
+            "ds_read_b64 v[92:93], %[xa] offset:48\n"
+            "ds_read_b64 v[94:95], %[xa] offset:56\n"
+            "1:\n"
+            "s_waitcnt lgkmcnt(7)\n"
+            "v_fmac_f32 %[acc], %[vc], v80\n"
+            "v_fmac_f32 %[acc], %[vc], v81\n"
+            "ds_read_b64 v[80:81], %[xa] offset:64\n"
+            "s_waitcnt lgkmcnt(7)\n"
+            "v_fmac_f32 %[acc], %[vc], v82\n"
+            "v_fmac_f32 %[acc], %[vc], v83\n"
+            "ds_read_b64 v[82:83], %[xa] offset:72\n"
+            "s_waitcnt lgkmcnt(7)\n"
+            "v_fmac_f32 %[acc], %[vc], v84\n"
+            "v_fmac_f32 %[acc], %[vc], v85\n"
+            "ds_read_b64 v[84:85], %[xa] offset:80\n"
+            "s_waitcnt lgkmcnt(7)\n"
+            "v_fmac_f32 %[acc], %[vc], v86\n"
+            "v_fmac_f32 %[acc], %[vc], v87\n"
+            "ds_read_b64 v[86:87], %[xa] offset:88\n"
+            "s_waitcnt lgkmcnt(7)\n"
+            "v_fmac_f32 %[acc], %[vc], v88\n"
+            "v_fmac_f32 %[acc], %[vc], v89\n"
+            "ds_read_b64 v[88:89], %[xa] offset:96\n"
+            "s_waitcnt lgkmcnt(7)\n"
+            "v_fmac_f32 %[acc], %[vc], v90\n"
+            "v_fmac_f32 %[acc], %[vc], v91\n"
+            "ds_read_b64 v[90:91], %[xa] offset:104\n"
+            "s_waitcnt lgkmcnt(7)\n"
+            "v_fmac_f32 %[acc], %[vc], v92\n"
+            "v_fmac_f32 %[acc], %[vc], v93\n"
+            "ds_read_b64 v[92:93], %[xa] offset:112\n"
+            "s_waitcnt lgkmcnt(7)\n"
+            "v_fmac_f32 %[acc], %[vc], v94\n"
+            "v_fmac_f32 %[acc], %[vc], v95\n"
+            "ds_read_b64 v[94:95], %[xa] offset:120\n"
+            "s_sub_u32 %[it], %[it], 1\n s_cmp_lg_u32 %[it], 0\n s_cbranch_scc1 1b\n"
+            "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [it] "+s"(it)
+        : [xa] "v"(xa), [va] "v"(va), [vc] "s"(vc)
+        : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "scc");
+    long long t1 = __builtin_amdgcn_s_memtime();
+    out[threadIdx.x] = acc;
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
+__global__ void ring_B64x14(float *out, long long *cyc, int iters, float vc) {
+    __shared__ __attribute__((aligned(16))) float x[64 * 260];
+    __shared__ __attribute__((aligned(16))) float v[512];
+    for (int i = threadIdx.x; i < 64 * 260; i += blockDim.x) x[i] = 1e-3f * (i % 97);
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) v[i] = 0.5f + 1e-3f * i;
+    __syncthreads();
+    typedef __attribute__((address_space(3))) const float lds_f;
+    uint32_t xa = (uint32_t)(size_t)(lds_f *)(&x[threadIdx.x * 260]);
+    uint32_t va = (uint32_t)(size_t)(lds_f *)(&v[0]);
+    float acc = 0;
+    int it = iters;
+    long long t0 = __builtin_amdgcn_s_memtime();
+    asm volatile(
+            "s_waitcnt lgkmcnt(0)\n"
+            "ds_read_b64 v[80:81], %[xa] offset:0\n"
+            "ds_read_b64 v[82:83], %[xa] offset:8\n"
+            "ds_read_b64 v[84:85], %[xa] offset:16\n"
+            "ds_read_b64 v[86:87], %[xa] offset:24\n"
+            "ds_read_b64 v[88:89], %[xa] offset:32\n"
+            "ds_read_b64 v[90:91], %[xa] offset:40\n"
+            "ds_read_b64 v[92:93], %[xa] offset:48\n"
+            "ds_read_b64 v[94:95], %[xa] offset:56\n"
+            "ds_read_b64 v[96:97], %[xa] offset:64\n"
+            "ds_read_b64 v[98:99], %[xa] offset:72\n"
+            "ds_read_b64 v[100:101], %[xa] offset:80\n"
+            "ds_read_b64 v[102:103], %[xa] offset:88\n"
+            "ds_read_b64 v[104:105], %[xa] offset:96\n"
+            "ds_read_b64 v[106:107], %[xa] offset:104\n"
+            "1:\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v80\n"
+            "v_fmac_f32 %[acc], %[vc], v81\n"
+            "ds_read_b64 v[80:81], %[xa] offset:112\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v82\n"
+            "v_fmac_f32 %[acc], %[vc], v83\n"
+            "ds_read_b64 v[82:83], %[xa] offset:120\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v84\n"
+            "v_fmac_f32 %[acc], %[vc], v85\n"
+            "ds_read_b64 v[84:85], %[xa] offset:128\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v86\n"
+            "v_fmac_f32 %[acc], %[vc], v87\n"
+            "ds_read_b64 v[86:87], %[xa] offset:136\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v88\n"
+            "v_fmac_f32 %[acc], %[vc], v89\n"
+            "ds_read_b64 v[88:89], %[xa] offset:144\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v90\n"
+            "v_fmac_f32 %[acc], %[vc], v91\n"
+            "ds_read_b64 v[90:91], %[xa] offset:152\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v92\n"
+            "v_fmac_f32 %[acc], %[vc], v93\n"
+            "ds_read_b64 v[92:93], %[xa] offset:160\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v94\n"
+            "v_fmac_f32 %[acc], %[vc], v95\n"
+            "ds_read_b64 v[94:95], %[xa] offset:168\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v96\n"
+            "v_fmac_f32 %[acc], %[vc], v97\n"
+            "ds_read_b64 v[96:97], %[xa] offset:176\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v98\n"
+            "v_fmac_f32 %[acc], %[vc], v99\n"
+            "ds_read_b64 v[98:99], %[xa] offset:184\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v100\n"
+            "v_fmac_f32 %[acc], %[vc], v101\n"
+            "ds_read_b64 v[100:101], %[xa] offset:192\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v102\n"
+            "v_fmac_f32 %[acc], %[vc], v103\n"
+            "ds_read_b64 v[102:103], %[xa] offset:200\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v104\n"
+            "v_fmac_f32 %[acc], %[vc], v105\n"
+            "ds_read_b64 v[104:105], %[xa] offset:208\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v106\n"
+            "v_fmac_f32 %[acc], %[vc], v107\n"
+            "ds_read_b64 v[106:107], %[xa] offset:216\n"
+            "s_sub_u32 %[it], %[it], 1\n s_cmp_lg_u32 %[it], 0\n s_cbranch_scc1 1b\n"
+            "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [it] "+s"(it)
+        : [xa] "v"(xa), [va] "v"(va), [vc] "s"(vc)
+        : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "scc");
+    long long t1 = __builtin_amdgcn_s_memtime();
+    out[threadIdx.x] = acc;
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
+__global__ void ring_B32x14(float *out, long long *cyc, int iters, float vc) {
+    __shared__ __attribute__((aligned(16))) float x[64 * 260];
+    __shared__ __attribute__((aligned(16))) float v[512];
+    for (int i = threadIdx.x; i < 64 * 260; i += blockDim.x) x[i] = 1e-3f * (i % 97);
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) v[i] = 0.5f + 1e-3f * i;
+    __syncthreads();
+    typedef __attribute__((address_space(3))) const float lds_f;
+    uint32_t xa = (uint32_t)(size_t)(lds_f *)(&x[threadIdx.x * 260]);
+    uint32_t va = (uint32_t)(size_t)(lds_f *)(&v[0]);
+    float acc = 0;
+    int it = iters;
+    long long t0 = __builtin_amdgcn_s_memtime();
+    asm volatile(
+            "s_waitcnt lgkmcnt(0)\n"
+            "ds_read_b32 v80, %[xa] offset:0\n"
+            "ds_read_b32 v81, %[xa] offset:4\n"
+            "ds_read_b32 v82, %[xa] offset:8\n"
+            "ds_read_b32 v83, %[xa] offset:12\n"
+            "ds_read_b32 v84, %[xa] offset:16\n"
+            "ds_read_b32 v85, %[xa] offset:20\n"
+            "ds_read_b32 v86, %[xa] offset:24\n"
+            "ds_read_b32 v87, %[xa] offset:28\n"
+            "ds_read_b32 v88, %[xa] offset:32\n"
+            "ds_read_b32 v89, %[xa] offset:36\n"
+            "ds_read_b32 v90, %[xa] offset:40\n"
+            "ds_read_b32 v91, %[xa] offset:44\n"
+            "ds_read_b32 v92, %[xa] offset:48\n"
+            "ds_read_b32 v93, %[xa] offset:52\n"
+            "1:\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v80\n"
+            "ds_read_b32 v80, %[xa] offset:56\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v81\n"
+            "ds_read_b32 v81, %[xa] offset:60\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v82\n"
+            "ds_read_b32 v82, %[xa] offset:64\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v83\n"
+            "ds_read_b32 v83, %[xa] offset:68\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v84\n"
+            "ds_read_b32 v84, %[xa] offset:72\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v85\n"
+            "ds_read_b32 v85, %[xa] offset:76\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v86\n"
+            "ds_read_b32 v86, %[xa] offset:80\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v87\n"
+            "ds_read_b32 v87, %[xa] offset:84\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v88\n"
+            "ds_read_b32 v88, %[xa] offset:88\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v89\n"
+            "ds_read_b32 v89, %[xa] offset:92\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v90\n"
+            "ds_read_b32 v90, %[xa] offset:96\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v91\n"
+            "ds_read_b32 v91, %[xa] offset:100\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v92\n"
+            "ds_read_b32 v92, %[xa] offset:104\n"
+            "s_waitcnt lgkmcnt(13)\n"
+            "v_fmac_f32 %[acc], %[vc], v93\n"
+            "ds_read_b32 v93, %[xa] offset:108\n"
+            "s_sub_u32 %[it], %[it], 1\n s_cmp_lg_u32 %[it], 0\n s_cbranch_scc1 1b\n"
+            "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [it] "+s"(it)
+        : [xa] "v"(xa), [va] "v"(va), [vc] "s"(vc)
+        : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "scc");
+    long long t1 = __builtin_amdgcn_s_memtime();
+    out[threadIdx.x] = acc;
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
+__global__ void ring_B64V7(float *out, long long *cyc, int iters, float vc) {
+    __shared__ __attribute__((aligned(16))) float x[64 * 260];
+    __shared__ __attribute__((aligned(16))) float v[512];
+    for (int i = threadIdx.x; i < 64 * 260; i += blockDim.x) x[i] = 1e-3f * (i % 97);
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) v[i] = 0.5f + 1e-3f * i;
+    __syncthreads();
+    typedef __attribute__((address_space(3))) const float lds_f;
+    uint32_t xa = (uint32_t)(size_t)(lds_f *)(&x[threadIdx.x * 260]);
+    uint32_t va = (uint32_t)(size_t)(lds_f *)(&v[0]);
+    float acc = 0;
+    int it = iters;
+    long long t0 = __builtin_amdgcn_s_memtime();
+    asm volatile(
+            "s_waitcnt lgkmcnt(0)\n"
+            "ds_read_b64 v[80:81], %[xa] offset:0\n"
+            "ds_read_b64 v[94:95], %[va] offset:0\n"
+            "ds_read_b64 v[82:83], %[xa] offset:8\n"
+            "ds_read_b64 v[96:97], %[va] offset:8\n"
+            "ds_read_b64 v[84:85], %[xa] offset:16\n"
+            "ds_read_b64 v[98:99], %[va] offset:16\n"
+            "ds_read_b64 v[86:87], %[xa] offset:24\n"
+            "ds_read_b64 v[100:101], %[va] offset:24\n"
+            "ds_read_b64 v[88:89], %[xa] offset:32\n"
+            "ds_read_b64 v[102:103], %[va] offset:32\n"
+            "ds_read_b64 v[90:91], %[xa] offset:40\n"
+            "ds_read_b64 v[104:105], %[va] offset:40\n"
+            "ds_read_b64 v[92:93], %[xa] offset:48\n"
+            "ds_read_b64 v[106:107], %[va] offset:48\n"
+            "1:\n"
+            "s_waitcnt lgkmcnt(12)\n"
+            "v_fmac_f32 %[acc], v94, v80\n"
+            "v_fmac_f32 %[acc], v95, v81\n"
+            "ds_read_b64 v[80:81], %[xa] offset:56\n"
+            "ds_read_b64 v[94:95], %[va] offset:56\n"
+            "s_waitcnt lgkmcnt(12)\n"
+            "v_fmac_f32 %[acc], v96, v82\n"
+            "v_fmac_f32 %[acc], v97, v83\n"
+            "ds_read_b64 v[82:83], %[xa] offset:64\n"
+            "ds_read_b64 v[96:97], %[va] offset:64\n"
+            "s_waitcnt lgkmcnt(12)\n"
+            "v_fmac_f32 %[acc], v98, v84\n"
+            "v_fmac_f32 %[acc], v99, v85\n"
+            "ds_read_b64 v[84:85], %[xa] offset:72\n"
+            "ds_read_b64 v[98:99], %[va] offset:72\n"
+            "s_waitcnt lgkmcnt(12)\n"
+            "v_fmac_f32 %[acc], v100, v86\n"
+            "v_fmac_f32 %[acc], v101, v87\n"
+            "ds_read_b64 v[86:87], %[xa] offset:80\n"
+            "ds_read_b64 v[100:101], %[va] offset:80\n"
+            "s_waitcnt lgkmcnt(12)\n"
+            "v_fmac_f32 %[acc], v102, v88\n"
+            "v_fmac_f32 %[acc], v103, v89\n"
+            "ds_read_b64 v[88:89], %[xa] offset:88\n"
+            "ds_read_b64 v[102:103], %[va] offset:88\n"
+            "s_waitcnt lgkmcnt(12)\n"
+            "v_fmac_f32 %[acc], v104, v90\n"
+            "v_fmac_f32 %[acc], v105, v91\n"
+            "ds_read_b64 v[90:91], %[xa] offset:96\n"
+            "ds_read_b64 v[104:105], %[va] offset:96\n"
+            "s_waitcnt lgkmcnt(12)\n"
+            "v_fmac_f32 %[acc], v106, v92\n"
+            "v_fmac_f32 %[acc], v107, v93\n"
+            "ds_read_b64 v[92:93], %[xa] offset:104\n"
+            "ds_read_b64 v[106:107], %[va] offset:104\n"
+            "s_sub_u32 %[it], %[it], 1\n s_cmp_lg_u32 %[it], 0\n s_cbranch_scc1 1b\n"
+            "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [it] "+s"(it)
+        : [xa] "v"(xa), [va] "v"(va), [vc] "s"(vc)
+        : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "scc");
+    long long t1 = __builtin_amdgcn_s_memtime();
+    out[threadIdx.x] = acc;
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
+int main4() {
+    float *out;
+    long long *cyc, h;
+    (void)hipMalloc(&out, 1024 * 4);
+    (void)hipMalloc(&cyc, 8);
+    const int iters = 20000;
+#define RUN4(K, NNZ, NAME)                                                                   \
+    for (int k = 0; k < 2; ++k)                                                              \
+        hipLaunchKernelGGL(K, dim3(1), dim3(64), 0, 0, out, cyc, iters, 0.5f);               \
+    (void)hipMemcpy(&h, cyc, 8, hipMemcpyDeviceToHost);                                      \
+    printf("{\"case\": \"%s\", \"cycles_per_nonzero\": %.2f}\n", NAME, (double)h / (iters * (double)(NNZ)));
+    RUN4(ring_B64x8, 16, "asm ring 8 x ds_read_b64 (2 nnz each), v in SGPR")
+    RUN4(ring_B64x14, 28, "asm ring 14 x ds_read_b64, v in SGPR")
+    RUN4(ring_B32x14, 14, "asm ring 14 x ds_read_b32, v in SGPR")
+    RUN4(ring_B64V7, 14, "asm ring 7 x (x ds_read_b64 + v ds_read_b64)")
+    return 0;
+}
+
 int main3() {
     float *out;
     long long *cyc, h;
@@ -489,7 +823,7 @@ int main3() {
     RUN(ring_X8, 8, "asm ring 8 batches: x b128, v in SGPR")
     RUN(ring_XV7, 7, "asm ring 7 batches: x b128 + v b128")
     RUN(ring_X12, 12, "asm ring 12 batches: x b128, v in SGPR")
-    return 0;
+    return main4();
 }
 
 int main2() {
