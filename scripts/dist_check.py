@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--row-chunks", type=int, default=1)
     ap.add_argument("--group-floats", type=int, default=0)
     ap.add_argument("--device", default="cuda", help="cpu: the CPU-twin rehearsal")
+    ap.add_argument("--cache", default=os.environ.get("TMPDIR", "/tmp"))
     args = ap.parse_args()
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -47,9 +48,25 @@ def main():
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "shapes.json")))[args.shape]
     spec = graphs.SHAPES[args.shape]
     t0 = time.time()
-    S = graphs.synthetic_graph(args.shape, seed=g["seed"])
-    X = torch.from_numpy(graphs.synthetic_features(args.shape, g["n"], g["features"],
-                                                   seed=g["feature_seed"])).to(dev)
+    # rank 0 generates the inputs once and shares them through .npy files
+    # (the RMAT shape takes minutes to generate; eight copies would thrash)
+    cache = os.path.join(args.cache, f"dist_check_{args.shape}")
+    names = ("row_ptr", "col_idx", "val", "X")
+    cached = all(os.path.exists(os.path.join(cache, nm + ".npy")) for nm in names)
+    if rank == 0 and not cached:
+        S = graphs.synthetic_graph(args.shape, seed=g["seed"])
+        Xh = graphs.synthetic_features(args.shape, g["n"], g["features"], seed=g["feature_seed"])
+        if world > 1:
+            os.makedirs(cache, exist_ok=True)
+            for name, arr in zip(names, (S.row_ptr, S.col_idx, S.val, Xh)):
+                np.save(os.path.join(cache, name + ".npy"), arr)
+    dist.barrier()
+    if rank != 0 or cached:
+        ld = lambda name: np.load(os.path.join(cache, name + ".npy"), mmap_mode="r")  # noqa: E731
+        S = graphs.CSRGraph(g["n"], ld("row_ptr"), ld("col_idx"), ld("val"))
+        Xh = ld("X")
+    X = torch.from_numpy(np.ascontiguousarray(Xh)).to(dev)
+    del Xh
     K = spec["hops"]
     if args.partition == "tiles":
         tp = TiledPropagator(S.row_ptr, S.col_idx, S.val, rank, world, args.col_blocks, dev,
@@ -65,8 +82,8 @@ def main():
         r0, r1 = shard.row_begin, shard.row_end
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    blocks = [None] * world
-    dist.all_gather_object(blocks, (r0, r1, mine.cpu().numpy()))
+    blocks = [None] * world if rank == 0 else None
+    dist.gather_object((r0, r1, mine.cpu().numpy()), blocks, dst=0)
     if rank == 0:
         Y = np.empty((g["n"], g["features"]), np.float32)
         covered = np.zeros(g["n"], bool)

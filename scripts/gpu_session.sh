@@ -36,12 +36,11 @@ for s in $STEPS; do
                 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
                 --dist-backend gloo ${DIST_ARGS} ;;
     dcheck) # 8 ranks on the one GPU (gloo, host-staged exchange): bit-exact X_K at full size
-            for v in "--partition rows" "--partition rows --row-chunks 4" \
-                     "--partition rows --group-floats 256" "--partition tiles --col-blocks 2" \
-                     "--partition tiles --col-blocks 4"; do
-              run dcheck timeout -k 10 400 python -m torch.distributed.run --nnodes=1 \
+            IFS=, read -ra VARIANTS <<< "${DCHECK_VARIANTS:---partition rows,--partition rows --row-chunks 4,--partition rows --group-floats 256,--partition tiles --col-blocks 2,--partition tiles --col-blocks 4}"
+            for v in "${VARIANTS[@]}"; do
+              run dcheck timeout -k 10 ${DCHECK_TIMEOUT:-400} python -m torch.distributed.run --nnodes=1 \
                   --nproc-per-node ${DCHECK_RANKS:-8} --master-addr 127.0.0.1 --master-port 29537 \
-                  scripts/dist_check.py --shape ${DCHECK_SHAPE:-reddit} $v
+                  scripts/dist_check.py --shape ${DCHECK_SHAPE:-reddit} $v --cache "${TMPDIR:-/tmp}"
               grep -h '^{' "$OUT/dcheck.log" >> "$OUT/dcheck_all.log"
             done ;;
     rdist)  run rdist timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
