@@ -204,9 +204,18 @@ int sgc_timing_collect(float *light_ms_host, float *hub_ms_host, int64_t capacit
  * several narrower launches): SGC_SPMM_NO_HUB = skip the plan's n_hub hub
  * rows (their Y rows are not written); SGC_SPMM_HUB_ONLY = only the hub rows,
  * on `stream` itself (no side stream).  The two launches together write
- * exactly what one unflagged launch writes. */
+ * exactly what one unflagged launch writes.
+ * Column-block passes (the multi-GPU pipeline that consumes an exchange in
+ * column order, sgc_amd.distributed.CyclicRowPropagator): SGC_SPMM_ACCUMULATE
+ * = each element's FMA chain starts from Y's current value instead of +0.0f,
+ * and rows without nonzeros in this CSR are left untouched.  When S's
+ * nonzeros are split by column range into CSRs S_0, S_1, ... (each row's
+ * nonzeros of S_g precede those of S_{g+1} in CSR order), one unflagged
+ * launch over S_0 followed by ACCUMULATE launches over S_1, S_2, ... writes
+ * exactly what one launch over S writes (the fp32 store/load between passes
+ * is exact). */
 enum { SGC_SPMM_X_PADDED = 1, SGC_SPMM_Y_PADDED = 2, SGC_SPMM_NO_HUB = 4,
-       SGC_SPMM_HUB_ONLY = 8 };
+       SGC_SPMM_HUB_ONLY = 8, SGC_SPMM_ACCUMULATE = 16 };
 int sgc_spmm_csr_f32_ex(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                         int64_t row_begin, int64_t row_end,
                         const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
@@ -275,6 +284,8 @@ int sgc_linear_xent_f32(const float *X, int64_t ldx, const float *W, const float
  * sgc_coo_to_csr_cpu: as sgc_coo_to_csr (stable by row, no coalescing;
  *   status bits 1/2/4), SGC_ERANGE on an out-of-range index.
  * sgc_spmm_csr_f32_cpu: as sgc_spmm_csr_f32 (utils.py:95), no plan.
+ * sgc_spmm_csr_f32_cpu_ex: with flags; SGC_SPMM_ACCUMULATE as on the GPU,
+ *   the padding flags accepted (and unused), the hub-split flags rejected.
  * sgc_propagate_f32_cpu: as sgc_propagate_f32 (utils.py:92-97); workspace
  *   = sgc_propagate_cpu_workspace(n_rows, F, K) bytes of host memory.
  * ------------------------------------------------------------------------- */
@@ -286,6 +297,10 @@ int sgc_spmm_csr_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const f
                          int64_t row_begin, int64_t row_end,
                          const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
                          int32_t n_threads);
+int sgc_spmm_csr_f32_cpu_ex(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                            int64_t row_begin, int64_t row_end,
+                            const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
+                            uint32_t flags, int32_t n_threads);
 int64_t sgc_propagate_cpu_workspace(int64_t n_rows, int64_t F, int32_t K);
 int sgc_propagate_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                           int64_t n_rows, const float *X0, int64_t ldx, float *out,

@@ -31,7 +31,9 @@ from sgc_amd.distributed import RowPartitionedPropagator, TiledPropagator, make_
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="reddit")
-    ap.add_argument("--partition", default="rows", choices=["rows", "tiles"])
+    ap.add_argument("--partition", default="rows", choices=["rows", "tiles", "cyclic"])
+    ap.add_argument("--groups", type=int, default=4, help="cyclic: column groups")
+    ap.add_argument("--tile", type=int, default=64, help="cyclic: rows per tile")
     ap.add_argument("--col-blocks", type=int, default=2)
     ap.add_argument("--row-chunks", type=int, default=1)
     ap.add_argument("--group-floats", type=int, default=0)
@@ -68,7 +70,15 @@ def main():
     X = torch.from_numpy(np.ascontiguousarray(Xh)).to(dev)
     del Xh
     K = spec["hops"]
-    if args.partition == "tiles":
+    row_index = None
+    if args.partition == "cyclic":
+        from sgc_amd.distributed import CyclicRowPropagator
+        cp = CyclicRowPropagator(S.row_ptr, S.col_idx, S.val, rank, world, dev, tile=args.tile,
+                                 groups=args.groups, host_staging=True)
+        mine = cp.propagate(X, K, output="sharded")
+        row_index = cp.row_index
+        r0, r1 = 0, 0
+    elif args.partition == "tiles":
         tp = TiledPropagator(S.row_ptr, S.col_idx, S.val, rank, world, args.col_blocks, dev,
                              group_floats=args.group_floats, host_staging=True)
         tp.prop.row_chunks = args.row_chunks
@@ -83,12 +93,16 @@ def main():
     if dev.type == "cuda":
         torch.cuda.synchronize()
     blocks = [None] * world if rank == 0 else None
-    dist.gather_object((r0, r1, mine.cpu().numpy()), blocks, dst=0)
+    dist.gather_object((r0, r1, row_index, mine.cpu().numpy()), blocks, dst=0)
     if rank == 0:
         Y = np.empty((g["n"], g["features"]), np.float32)
         covered = np.zeros(g["n"], bool)
-        for a, b, arr in blocks:
-            if b > a and not covered[a:b].any():  # tiles: C ranks share a row block
+        for a, b, ri, arr in blocks:
+            if ri is not None:  # cyclic: the rank's rows by global id
+                assert not covered[ri].any()
+                Y[ri] = arr
+                covered[ri] = True
+            elif b > a and not covered[a:b].any():  # tiles: C ranks share a row block
                 Y[a:b] = arr
                 covered[a:b] = True
         ok = bool(covered.all()) and hashlib.sha256(Y.tobytes()).hexdigest() == \
@@ -96,7 +110,9 @@ def main():
         print(json.dumps({"shape": args.shape, "world": world, "partition": args.partition,
                           "col_blocks": args.col_blocks if args.partition == "tiles" else 1,
                           "row_chunks": args.row_chunks, "group_floats": args.group_floats,
-                          "rows_per_rank": [int(b - a) for a, b, _ in blocks],
+                          "groups": args.groups if args.partition == "cyclic" else None,
+                          "rows_per_rank": [int(b - a) if ri is None else int(len(ri))
+                                            for a, b, ri, _ in blocks],
                           "bit_exact_vs_reference_hash": ok,
                           "seconds": round(time.time() - t0, 1)}), flush=True)
     dist.barrier()

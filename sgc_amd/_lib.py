@@ -60,6 +60,8 @@ SIGNATURES = {
                                           ctypes.POINTER(_u32)]),
     "sgc_spmm_csr_f32_cpu": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
                                             _i32]),
+    "sgc_spmm_csr_f32_cpu_ex": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
+                                               ctypes.c_uint32, _i32]),
     "sgc_propagate_cpu_workspace": (_i64, [_i64, _i64, _i32]),
     "sgc_propagate_f32_cpu": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _i32,
                                              _p, _i64, _i32]),

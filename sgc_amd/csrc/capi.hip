@@ -62,7 +62,7 @@ int coo_to_csr_cpu(const int64_t *rows, const int64_t *cols, const float *vals, 
                    float *val_out, uint32_t *status_host);
 int spmm_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val, int64_t row_begin,
              int64_t row_end, const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
-             int32_t n_threads);
+             int32_t n_threads, bool accum);
 int64_t propagate_cpu_workspace(int64_t n_rows, int64_t F, int32_t K);
 int propagate_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                   int64_t n_rows, const float *X0, int64_t ldx, float *out, int64_t ldo, int64_t F,
@@ -177,7 +177,7 @@ int sgc_spmm_csr_f32_ex(const int32_t *row_ptr, const int32_t *col_idx, const fl
                         int64_t ldy, int64_t F, const int32_t *plan, int64_t n_heavy,
                         int64_t n_hub, int32_t heavy_threshold, uint32_t flags, void *stream) {
     constexpr uint32_t known = SGC_SPMM_X_PADDED | SGC_SPMM_Y_PADDED | SGC_SPMM_NO_HUB |
-                               SGC_SPMM_HUB_ONLY;
+                               SGC_SPMM_HUB_ONLY | SGC_SPMM_ACCUMULATE;
     SGC_REQUIRE((flags & ~known) == 0, SGC_EINVAL, "spmm_ex: unknown flags 0x%x", flags);
     SGC_REQUIRE(!((flags & SGC_SPMM_NO_HUB) && (flags & SGC_SPMM_HUB_ONLY)), SGC_EINVAL,
                 "spmm_ex: NO_HUB and HUB_ONLY together");
@@ -287,7 +287,18 @@ int sgc_coo_to_csr_cpu(const int64_t *rows, const int64_t *cols, const float *va
 int sgc_spmm_csr_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                          int64_t row_begin, int64_t row_end, const float *X, int64_t ldx,
                          float *Y, int64_t ldy, int64_t F, int32_t n_threads) {
-    return spmm_cpu(row_ptr, col_idx, val, row_begin, row_end, X, ldx, Y, ldy, F, n_threads);
+    return spmm_cpu(row_ptr, col_idx, val, row_begin, row_end, X, ldx, Y, ldy, F, n_threads,
+                    false);
+}
+
+int sgc_spmm_csr_f32_cpu_ex(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                            int64_t row_begin, int64_t row_end, const float *X, int64_t ldx,
+                            float *Y, int64_t ldy, int64_t F, uint32_t flags, int32_t n_threads) {
+    // the padding flags only license wider GPU loads; the CPU reads exactly F
+    constexpr uint32_t known = SGC_SPMM_X_PADDED | SGC_SPMM_Y_PADDED | SGC_SPMM_ACCUMULATE;
+    SGC_REQUIRE((flags & ~known) == 0, SGC_EINVAL, "spmm_cpu_ex: unsupported flags 0x%x", flags);
+    return spmm_cpu(row_ptr, col_idx, val, row_begin, row_end, X, ldx, Y, ldy, F, n_threads,
+                    (flags & SGC_SPMM_ACCUMULATE) != 0);
 }
 
 int64_t sgc_propagate_cpu_workspace(int64_t n_rows, int64_t F, int32_t K) {

@@ -5,6 +5,8 @@
 // the drop-in must too.  This is product code, not the test oracle: the same
 // numerical contract as the HIP kernels --
 //     Y[i, f]: acc = +0.0f; for k in row i (CSR order): acc = fmaf(val[k], X[col[k], f], acc)
+// (with SGC_SPMM_ACCUMULATE the chain starts from Y[i, f] instead: a later
+// column-block pass of the same rows, include/sgc_amd.h)
 // -- which is bit-identical to torch.spmm's CPU COO kernel.  Threads own whole
 // rows (never a split (row, feature) sum); within a row the feature loop
 // vectorises across independent chains (vfmadd, one chain per SIMD lane), so
@@ -31,8 +33,10 @@ constexpr int64_t kRowsPerTask = 64;
 __attribute__((always_inline)) inline void row_fma(const int32_t *__restrict__ col,
                                                    const float *__restrict__ val, int64_t k0,
                                                    int64_t k1, const float *__restrict__ X,
-                                                   int64_t ldx, float *__restrict__ y, int64_t F) {
-    for (int64_t f = 0; f < F; ++f) y[f] = 0.0f;
+                                                   int64_t ldx, float *__restrict__ y, int64_t F,
+                                                   bool accum) {
+    if (!accum)
+        for (int64_t f = 0; f < F; ++f) y[f] = 0.0f;
     for (int64_t k = k0; k < k1; ++k) {
         const float v = val[k];
         const float *__restrict__ xr = X + (int64_t)col[k] * ldx;
@@ -41,24 +45,25 @@ __attribute__((always_inline)) inline void row_fma(const int32_t *__restrict__ c
 }
 
 using RowFn = void (*)(const int32_t *, const float *, int64_t, int64_t, const float *, int64_t,
-                       float *, int64_t);
+                       float *, int64_t, bool);
 
 __attribute__((target("avx512f,avx512vl,fma"))) void row_avx512(
     const int32_t *col, const float *val, int64_t k0, int64_t k1, const float *X, int64_t ldx,
-    float *y, int64_t F) {
-    row_fma(col, val, k0, k1, X, ldx, y, F);
+    float *y, int64_t F, bool accum) {
+    row_fma(col, val, k0, k1, X, ldx, y, F, accum);
 }
 
 __attribute__((target("avx2,fma"))) void row_avx2(const int32_t *col, const float *val,
                                                   int64_t k0, int64_t k1, const float *X,
-                                                  int64_t ldx, float *y, int64_t F) {
-    row_fma(col, val, k0, k1, X, ldx, y, F);
+                                                  int64_t ldx, float *y, int64_t F, bool accum) {
+    row_fma(col, val, k0, k1, X, ldx, y, F, accum);
 }
 
 // No hardware FMA: fmaf from libm (correctly rounded, so still bit-exact).
 void row_generic(const int32_t *col, const float *val, int64_t k0, int64_t k1, const float *X,
-                 int64_t ldx, float *y, int64_t F) {
-    for (int64_t f = 0; f < F; ++f) y[f] = 0.0f;
+                 int64_t ldx, float *y, int64_t F, bool accum) {
+    if (!accum)
+        for (int64_t f = 0; f < F; ++f) y[f] = 0.0f;
     for (int64_t k = k0; k < k1; ++k) {
         const float v = val[k];
         const float *xr = X + (int64_t)col[k] * ldx;
@@ -153,7 +158,7 @@ int coo_to_csr_cpu(const int64_t *rows, const int64_t *cols, const float *vals, 
 
 int spmm_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val, int64_t row_begin,
              int64_t row_end, const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
-             int32_t n_threads) {
+             int32_t n_threads, bool accum) {
     SGC_REQUIRE(row_ptr && X && Y, SGC_EINVAL, "spmm_cpu: null pointer");
     SGC_REQUIRE(row_begin >= 0 && row_end >= row_begin && row_end < INT32_MAX, SGC_ERANGE,
                 "spmm_cpu: bad row range [%lld, %lld)", (long long)row_begin, (long long)row_end);
@@ -169,7 +174,8 @@ int spmm_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val, i
         const int64_t r0 = row_begin + t * kRowsPerTask;
         const int64_t r1 = std::min(row_end, r0 + kRowsPerTask);
         for (int64_t r = r0; r < r1; ++r)
-            row(col_idx, val, row_ptr[r], row_ptr[r + 1], X, ldx, Y + (r - row_begin) * ldy, F);
+            row(col_idx, val, row_ptr[r], row_ptr[r + 1], X, ldx, Y + (r - row_begin) * ldy, F,
+                accum);
     });
     return SGC_OK;
 }
@@ -202,7 +208,8 @@ int propagate_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *v
         const bool last = h == K - 1;
         float *dst = last ? out : bufs[h & 1];
         const int64_t ldd = last ? ldo : F;
-        const int rc = spmm_cpu(row_ptr, col_idx, val, 0, n_rows, src, lds, dst, ldd, F, n_threads);
+        const int rc = spmm_cpu(row_ptr, col_idx, val, 0, n_rows, src, lds, dst, ldd, F, n_threads,
+                                 false);
         if (rc) return rc;
         src = dst;
         lds = ldd;

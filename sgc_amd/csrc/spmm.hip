@@ -4,8 +4,11 @@
 // Numerical contract (pinned by tests/golden): every output
 // element is ONE sequential fp32 FMA chain over its row's nonzeros in CSR
 // order, starting from +0.0f.  So a lane owns features and walks the row's
-// nonzeros in order; no (row, feature) sum is ever split across lanes, waves
-// or launches.
+// nonzeros in order; no (row, feature) sum is ever split across lanes or
+// waves.  The one split is across launches, in order: with
+// SGC_SPMM_ACCUMULATE a launch over column block g of S continues each chain
+// from the fp32 value block g-1's launch stored (an exact round trip), so the
+// passes over blocks 0, 1, ... of a row's CSR-ordered nonzeros are one chain.
 //
 // Mapping (one wavefront = 64 lanes per work item):
 //   * features are cut into slices of 64*C*V floats (grid y); each slice is
@@ -51,8 +54,9 @@ __device__ __forceinline__ void row_chunks(const int *__restrict__ col,
                                            const float *__restrict__ val, int k0, int k1,
                                            const float *__restrict__ X, int64_t ldx,
                                            float *__restrict__ yrow, int F, int chunk0,
-                                           int lane) {
+                                           int lane, bool accum) {
     using VT = typename Vec<V>::T;
+    if (accum && k1 == k0) return;  // nothing to add: the row keeps its partial chains
     uint32_t boff[C];
     bool ok[C];
 #pragma unroll
@@ -66,6 +70,12 @@ __device__ __forceinline__ void row_chunks(const int *__restrict__ col,
     for (int c = 0; c < C; ++c)
 #pragma unroll
         for (int v = 0; v < V; ++v) set_elem<V>(acc[c], v, 0.0f);
+    if (accum) {  // continue the chains an earlier column-block pass stored
+        const char *Yr = reinterpret_cast<const char *>(yrow);
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if (ok[c]) acc[c] = *reinterpret_cast<const VT *>(Yr + boff[c]);
+    }
 
     const char *Xb = reinterpret_cast<const char *>(X);
     const int64_t row_bytes = ldx * 4;
@@ -154,10 +164,11 @@ __device__ __forceinline__ void row_chunks_pipe(const int *__restrict__ col,
                                                 const float *__restrict__ val, int k0, int k1,
                                                 const float *__restrict__ X, int64_t ldx,
                                                 float *__restrict__ yrow, int F, int chunk0,
-                                                int lane) {
+                                                int lane, bool accum) {
     using VT = typename Vec<V>::T;
     constexpr int kSteps = kWave / U;  // steps per 64-nonzero block
     static_assert(kWave % U == 0 && kSteps % 2 == 0, "U must divide 64 into an even count");
+    if (accum && k1 == k0) return;  // nothing to add: the row keeps its partial chains
     uint32_t boff[C];
     bool ok[C];
 #pragma unroll
@@ -171,6 +182,12 @@ __device__ __forceinline__ void row_chunks_pipe(const int *__restrict__ col,
     for (int c = 0; c < C; ++c)
 #pragma unroll
         for (int v = 0; v < V; ++v) set_elem<V>(acc[c], v, 0.0f);
+    if (accum) {  // continue the chains an earlier column-block pass stored
+        const char *Yr = reinterpret_cast<const char *>(yrow);
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if (ok[c]) acc[c] = *reinterpret_cast<const VT *>(Yr + boff[c]);
+    }
 
     if (k1 > k0) {
         const char *Xb = reinterpret_cast<const char *>(X);
@@ -264,7 +281,7 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
     int row_begin, int n_rows, int F, const int *__restrict__ heavy_rows, int n_heavy,
-    int heavy_threshold) {
+    int heavy_threshold, int accum) {
     constexpr int VH = (SGC_HEAVY_VEC < V) ? SGC_HEAVY_VEC : V;  // heavy lanes' vector width
     constexpr int kSub = C * V / VH;  // 64*VH-float sub-chunks per slice (heavy items)
     const int lane = threadIdx.x & (kWave - 1);
@@ -280,10 +297,11 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
         const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
 #if SGC_PIPE
         row_chunks_pipe<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
-                                        Y + (int64_t)(row - row_begin) * ldy, F, sub, lane);
+                                        Y + (int64_t)(row - row_begin) * ldy, F, sub, lane,
+                                        accum != 0);
 #else
         row_chunks<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
-                                   Y + (int64_t)(row - row_begin) * ldy, F, sub, lane);
+                                   Y + (int64_t)(row - row_begin) * ldy, F, sub, lane, accum != 0);
 #endif
         return;
     }
@@ -293,9 +311,11 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
     if (k1 - k0 > heavy_threshold) return;  // done as a heavy item or by the hub kernel
 #if SGC_PIPE
-    row_chunks_pipe<V, C, U>(col, val, k0, k1, X, ldx, Y + (int64_t)r * ldy, F, slice * C, lane);
+    row_chunks_pipe<V, C, U>(col, val, k0, k1, X, ldx, Y + (int64_t)r * ldy, F, slice * C, lane,
+                             accum != 0);
 #else
-    row_chunks<V, C, U>(col, val, k0, k1, X, ldx, Y + (int64_t)r * ldy, F, slice * C, lane);
+    row_chunks<V, C, U>(col, val, k0, k1, X, ldx, Y + (int64_t)r * ldy, F, slice * C, lane,
+                        accum != 0);
 #endif
 }
 
@@ -329,7 +349,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
     int row_begin, int n_rows, int F, int F_load, int LR, int vec_store, int n_sub,
-    const int *__restrict__ heavy_rows, int n_heavy, int heavy_threshold) {
+    const int *__restrict__ heavy_rows, int n_heavy, int heavy_threshold, int accum) {
     constexpr int V = 4, U = kRowsU;
     constexpr int kSteps = LB / U;  // steps per LDS block
     static_assert(kSteps >= 2 && kSteps % 2 == 0, "bad block");
@@ -349,7 +369,8 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
         const int row = heavy_rows[h];
         const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
         row_chunks_pipe<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
-                                        Y + (int64_t)(row - row_begin) * ldy, F, sub, lane);
+                                        Y + (int64_t)(row - row_begin) * ldy, F, sub, lane,
+                                        accum != 0);
         return;
     }
     const int R = kWave / LR;  // rows per wave (uniform)
@@ -372,6 +393,19 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const uint32_t boff = ok ? uint32_t(f) * 4u : 0u;
     const int lds_row = (sub < R ? sub : 0) * LB;  // this lane's row block in LDS
     f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    // accumulate: continue the chains an earlier column-block pass stored;
+    // rows without nonzeros in this pass are neither read nor written
+    const bool store = mine && ok && (!accum || len > 0);
+    if (accum && store) {
+        const float *yr = Y + (int64_t)r * ldy;
+        if (vec_store) {
+            acc = *reinterpret_cast<const f4 *>(yr + f);
+        } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if (f + v < F) acc[v] = yr[f + v];
+        }
+    }
     if (n_max > 0) {
         const char *Xb = reinterpret_cast<const char *>(X);
         const int64_t row_bytes = ldx * 4;
@@ -443,7 +477,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
             fetch(base + 2 * LB, colB, valB);
         }
     }
-    if (mine && ok) {
+    if (store) {
         float *yr = Y + (int64_t)r * ldy;
         if (vec_store) {
             *reinterpret_cast<f4 *>(yr + f) = acc;
@@ -625,7 +659,7 @@ template <int HC>
 __global__ __launch_bounds__(1024) void spmm_hub_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy, int row_begin,
-    int F, const int *__restrict__ hub_rows, int n_chunks) {
+    int F, const int *__restrict__ hub_rows, int n_chunks, int accum) {
     using Sh = HubShape<HC>;
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) float gxT[2][HC * Sh::kStride];  // 2 x 66.5 KB
@@ -701,6 +735,7 @@ __global__ __launch_bounds__(1024) void spmm_hub_kernel(
     if (SGC_HUB_PRIO && w == 0) __builtin_amdgcn_s_setprio(SGC_HUB_PRIO);
     __syncthreads();
     float acc = 0.0f;
+    if (accum && w == 0 && f < F) acc = Y[(int64_t)(row - row_begin) * ldy + f];
     for (int r0 = 0; r0 < n_round; r0 += kHubUnroll) {
 #pragma unroll
         for (int s = 0; s < kHubUnroll; ++s) {
@@ -853,6 +888,7 @@ struct LaunchArgs {
     const int *heavy_rows;
     int n_heavy, heavy_threshold;
     int slices;
+    int accum;
     hipStream_t stream;
 };
 
@@ -950,7 +986,7 @@ hipError_t launch_vc(const LaunchArgs &a) {
     dim3 grid((unsigned)blocks, (unsigned)a.slices);
     hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH>), grid, dim3(kBlock), g_light_lds, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin, a.n_rows,
-                       a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold);
+                       a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold, a.accum);
     return hipGetLastError();
 }
 
@@ -988,7 +1024,7 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, SGC_HEAVY_U>), grid, dim3(kBlock), g_light_lds,
                        a.stream, a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
                        a.n_rows, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
-                       a.heavy_threshold);
+                       a.heavy_threshold, a.accum);
     return hipGetLastError();
 }
 
@@ -1104,6 +1140,7 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     }
     const bool hub_only = (flags & SGC_SPMM_HUB_ONLY) != 0;
     if (hub_only && n_hub == 0) return SGC_OK;
+    const int accum = (flags & SGC_SPMM_ACCUMULATE) ? 1 : 0;
     SideStream *side = nullptr;
     std::unique_lock<std::mutex> side_lock;
     std::unique_lock<std::mutex> timing_lock(g_timing_mu);
@@ -1137,11 +1174,11 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         if (hc == 32)
             hipLaunchKernelGGL(spmm_hub_kernel<32>, dim3((unsigned)(n_hub * n_chunks)), dim3(1024),
                                0, hs, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
-                               (int)F, heavy_rows, n_chunks);
+                               (int)F, heavy_rows, n_chunks, accum);
         else
             hipLaunchKernelGGL(spmm_hub_kernel<64>, dim3((unsigned)(n_hub * n_chunks)), dim3(1024),
                                0, hs, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
-                               (int)F, heavy_rows, n_chunks);
+                               (int)F, heavy_rows, n_chunks, accum);
         SGC_HIP_CHECK(hipGetLastError());
         if (timing) SGC_HIP_CHECK(hipEventRecord(tl.h1, hs));
         heavy_rows += n_hub;
@@ -1159,7 +1196,7 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     }
 
     LaunchArgs a{row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)n_rows, (int)F,
-                 heavy_rows, (int)n_heavy, heavy_threshold, 0, light_stream};
+                 heavy_rows, (int)n_heavy, heavy_threshold, 0, accum, light_stream};
     // 16-B lanes over F rounded up to 4 columns: X rows must be 16-B aligned
     // and readable that far (flag SGC_SPMM_X_PADDED unless F % 4 == 0)
     const int64_t F4 = (F + 3) / 4 * 4;

@@ -521,6 +521,372 @@ class RowPartitionedPropagator:
 
 
 # ---------------------------------------------------------------------------
+# Cyclic row partition with column-ordered exchange (SURVEY.md 8(e) overlap).
+
+@dataclass
+class CyclicShard:
+    """One rank's rows of S under the cyclic tiling of CyclicRowPropagator.
+
+    Rows are cut into tiles of `tile` consecutive rows; tile t*P + p goes to
+    rank p, for rounds t = 0..T-1, T = G*Tg (rows past n are empty padding).
+    Rank p's local row t*tile + i is global row (t*P + p)*tile + i, so its
+    local rows are in ascending global order, and the rounds of column group g
+    (t in [g*Tg, (g+1)*Tg)) cover the contiguous global range
+    [g*Tg*P*tile, (g+1)*Tg*P*tile) -- held by ALL ranks in equal parts.
+
+    csr_input: the rank's rows with global column ids (hop 1 reads X_0).
+    sub[g]: the same rows restricted to column group g, with columns remapped
+    to rows of the exchange buffer (see gathered_index); each row's nonzeros of
+    group g are a contiguous run of its CSR-ordered nonzeros, so passes over
+    g = 0, 1, ... in order are the row's FMA chain in CSR order."""
+    rank: int
+    world_size: int
+    n: int
+    tile: int
+    groups: int
+    rounds_per_group: int
+    global_rows: np.ndarray          # int64 [T*tile] global id of each local row
+    n_valid: int                     # local rows with global id < n (a prefix)
+    csr_input: "object"              # DeviceCSR over [T*tile] rows, global columns
+    sub: list                        # [G] DeviceCSR over [T*tile] rows, gathered columns
+    nnz: int
+
+    @property
+    def rows(self):
+        """Local rows, padding included (every launch covers all of them)."""
+        return int(self.global_rows.shape[0])
+
+    @property
+    def group_rows(self):
+        """Local rows per column group (= rows each rank sends per all-gather)."""
+        return self.rounds_per_group * self.tile
+
+    @property
+    def gathered_rows(self):
+        return self.world_size * self.rows
+
+
+def cyclic_layout(n, world_size, tile, groups):
+    """(rounds per group Tg, rounds T = groups*Tg) covering n rows."""
+    tiles = max(1, -(-n // tile))
+    rounds = -(-tiles // world_size)
+    Tg = max(1, -(-rounds // groups))
+    return Tg, groups * Tg
+
+
+def cyclic_gathered_index(j, world_size, tile, Tg):
+    """Exchange-buffer row of global node j: group g's all-gather lands rank
+    q's Tg tiles at rows [(g*P + q)*Tg*tile, ...), tile t' (within the group)
+    at offset t'*tile."""
+    j = np.asarray(j, dtype=np.int64)
+    P, b = world_size, tile
+    t = j // (P * b)
+    q = (j // b) % P
+    i = j % b
+    g, tl = t // Tg, t % Tg
+    return ((g * P + q) * Tg + tl) * b + i
+
+
+def make_cyclic_shard(row_ptr, col_idx, val, rank, world_size, device, tile=64, groups=4):
+    """Host (numpy) slicing of S for `rank` under the cyclic tiling, moved to
+    `device` as DeviceCSRs (hop-1 CSR + one per column group)."""
+    from .propagate import DeviceCSR
+    row_ptr = np.asarray(row_ptr, dtype=np.int64)
+    n = int(row_ptr.shape[0] - 1)
+    P, b, G = int(world_size), int(tile), int(groups)
+    if P < 1 or b < 1 or G < 1:
+        raise ValueError("world_size, tile and groups must be >= 1")
+    Tg, T = cyclic_layout(n, P, b, G)
+    if P * T * b >= 2**31:
+        raise ValueError("cyclic exchange buffer exceeds int32 row ids")
+    t = np.arange(T, dtype=np.int64)
+    starts = (t * P + rank) * b                         # global first row of each local tile
+    grows = (starts[:, None] + np.arange(b, dtype=np.int64)[None, :]).reshape(-1)
+    valid = grows < n
+    n_valid = int(valid.sum())
+    gv = grows[:n_valid]                                # valid local rows are a prefix
+    deg = np.zeros(T * b, dtype=np.int64)
+    deg[:n_valid] = row_ptr[gv + 1] - row_ptr[gv]
+    lrp = np.zeros(T * b + 1, dtype=np.int64)
+    np.cumsum(deg, out=lrp[1:])
+    nnz = int(lrp[-1])
+    # nonzeros of each local tile are one contiguous range of the global CSR
+    t0 = np.minimum(starts, n)
+    t1 = np.minimum(starts + b, n)
+    k0, k1 = row_ptr[t0], row_ptr[t1]
+    lens = k1 - k0
+    idx = np.repeat(k0 - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + \
+        np.arange(nnz, dtype=np.int64)
+    cols = np.asarray(col_idx)[idx].astype(np.int64)
+    vals = np.asarray(val)[idx].astype(np.float32)
+    del idx
+    gcols = cyclic_gathered_index(cols, P, b, Tg)
+    grp = cols // (P * b * Tg)                          # column group of each nonzero
+    local_row = np.repeat(np.arange(T * b, dtype=np.int64), deg)
+    if G > 1 and nnz > 1:
+        # the passes visit groups 0, 1, ...: a row's CSR order must not go back
+        # to an earlier group (any column-sorted CSR -- the reference's scipy S
+        # -- qualifies; storage-order COO with unsorted rows may not)
+        back = (np.diff(grp) < 0) & (local_row[1:] == local_row[:-1])
+        if back.any():
+            i = int(local_row[1:][back][0])
+            raise ValueError(
+                f"CyclicRowPropagator: row {int(grows[i])}'s nonzeros are not in ascending "
+                f"column-group order, so column-group passes would reorder its FMA chain; "
+                f"use groups=1 or another partition for this CSR")
+    counts = np.bincount(local_row * G + grp, minlength=T * b * G).reshape(T * b, G)
+    del local_row
+    order = np.argsort(grp, kind="stable")              # group-major, CSR order within
+
+    def dev(a, dt):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dt)
+
+    csr_input = DeviceCSR(T * b, n, dev(lrp, torch.int32), dev(cols, torch.int32),
+                          dev(vals, torch.float32))
+    sub, off = [], 0
+    for g in range(G):
+        rp = np.zeros(T * b + 1, dtype=np.int64)
+        np.cumsum(counts[:, g], out=rp[1:])
+        sel = order[off:off + int(rp[-1])]
+        off += int(rp[-1])
+        sub.append(DeviceCSR(T * b, P * T * b, dev(rp, torch.int32), dev(gcols[sel], torch.int32),
+                             dev(vals[sel], torch.float32)))
+    return CyclicShard(rank, P, n, b, G, Tg, grows, n_valid, csr_input, sub, nnz)
+
+
+def _pad_columns_allocated(t):
+    """Columns [F, round4(F)) of every row of the 2-D view t lie inside its
+    storage (F % 4 != 0 only: otherwise there is nothing to pad)."""
+    rows, F = t.shape
+    F4 = -(-F // 4) * 4
+    if F4 == F or rows == 0 or t.stride(1) != 1 or t.stride(0) < F4:
+        return False
+    end = t.storage_offset() + (rows - 1) * t.stride(0) + F4
+    return end * t.element_size() <= t.untyped_storage().nbytes()
+
+
+def _cyclic_spmm(csr, X, out, rows, accumulate, part="all"):
+    """Rows [r0, r1) of csr . X into out[r0:r1] through the product engine;
+    accumulate = continue the chains stored in out (SPMM_ACCUMULATE); part =
+    "all", or the split launch "light" (all but the hub rows) / "hub"."""
+    from . import _lib
+    from .propagate import (SPMM_ACCUMULATE, SPMM_HUB_ONLY, SPMM_NO_HUB, SPMM_X_PADDED,
+                            SPMM_Y_PADDED, SpmmLaunch, spmm)
+    r0, r1 = rows
+    flags = (SPMM_ACCUMULATE if accumulate else 0) | \
+        {"all": 0, "light": SPMM_NO_HUB, "hub": SPMM_HUB_ONLY}[part]
+    if X.shape[1] < out.shape[1]:
+        raise ValueError("output wider than input")
+    if not X.is_cuda:
+        return spmm(csr, X, r0, r1, out=out[r0:r1], flags=flags)
+    # the engine's own buffers have 128-B rows: let the kernel use 16-B lanes
+    # (columns [F, round4(F)) of every row allocated; their values unused)
+    if _pad_columns_allocated(X):
+        flags |= SPMM_X_PADDED
+    if _pad_columns_allocated(out):
+        flags |= SPMM_Y_PADDED
+    launches = csr.__dict__.setdefault("_launches", {})
+    key = (r0, r1, flags, X.data_ptr(), tuple(X.shape), X.stride(0), out.data_ptr(),
+           tuple(out.shape), out.stride(0))
+    fn = launches.get(key)
+    if fn is None:
+        if len(launches) > 256:
+            launches.clear()
+        fn = launches[key] = SpmmLaunch(csr, X, out[r0:r1], r0, r1, flags)
+    fn(_lib.stream_handle(X.device))
+    return out
+
+
+class CyclicRowPropagator:
+    """X_K = S^K X_0 with S's rows dealt out in tiles, round-robin over the
+    ranks, and the next hop consuming the exchange column group by column
+    group as it arrives -- SURVEY.md 8(e)'s overlap, built for a point-to-
+    point xGMI mesh.
+
+    Why cyclic.  Hop k+1 may add row i's nonzeros only in CSR (ascending
+    column) order, so it can start on the part of X_k whose columns come
+    first.  With contiguous row blocks the first columns all live on rank 0,
+    and delivering them first would leave 6 of every GPU's 7 links idle.
+    With tiles dealt round-robin, the first Tg*P tiles of X_k -- the first
+    column group -- are spread evenly over ALL ranks: the exchange is G
+    ordinary all-gathers (every link busy), and all-gather g delivers exactly
+    column group g.
+
+    Per hop (GPU; G = `groups`):
+      * hop 1 reads the caller's X_0 (global column ids) in one pass;
+      * hop k >= 2 runs G passes over the rank's rows: pass g uses only the
+        nonzeros of column group g, waits only for all-gather g of X_{k-1},
+        and continues the FMA chains pass g-1 stored (SGC_SPMM_ACCUMULATE:
+        one fp32 store/load per element between passes -- exact, so the
+        result is bit-identical to one pass);
+      * when the hop's output is exchanged, its final pass runs in G row
+        chunks (local rows of column group c) and all-gather c is issued on
+        the comm stream as soon as chunk c is done -- so the exchange of X_k
+        overlaps hop k's own tail AND hop k+1's passes over earlier groups.
+    Costs: the accumulator round trip (2 x 4F bytes per row per extra pass)
+    and G launches per hop instead of one; the gain is that the next hop's
+    passes read X from one column group at a time (1/G of X_k live: better
+    L2 / Infinity Cache reuse than a full-width pass over all of X_k).
+
+    output="sharded": this rank's rows of X_K, in ascending global order,
+    global ids in `row_index` (valid rows only).  output="replicated": X_K
+    [N, F] on every rank.  spmm_fn(csr, X, out, rows, accumulate, part)
+    computes out[rows] (default: the HIP engine on ROCm tensors, the CPU twin
+    on CPU tensors).
+
+    Hub rows: hop 1's row chunks run as split launches (every row but the hub
+    rows on the compute stream, the hub rows on a hub stream; all-gather c
+    waits for both), so a 0.3-ms hub chain in chunk c does not hold back chunk
+    c+1.  The column-group passes keep each launch's hub kernel joined: a row
+    that is a hub of pass g may be a light row of pass g+1, which must not
+    start on it before pass g's chain has stored."""
+
+    def __init__(self, row_ptr, col_idx, val, rank, world_size, device, group=None,
+                 tile=64, groups=4, host_staging=False, spmm_fn: Optional[Callable] = None,
+                 pad_input: Optional[bool] = None):
+        self.shard = make_cyclic_shard(row_ptr, col_idx, val, rank, world_size, device, tile,
+                                       groups)
+        self.group = group
+        self.host_staging = host_staging
+        self.spmm_fn = spmm_fn or _cyclic_spmm
+        self.pad_input = pad_input
+        self._bufs = {}
+        self._comm = None
+        self._hub = None
+        self._events = {}
+
+    @property
+    def row_index(self):
+        return self.shard.global_rows[:self.shard.n_valid]
+
+    def _buf(self, key, shape, like):
+        b = self._bufs.get(key)
+        if b is None or tuple(b.shape) != tuple(shape) or b.device != like.device:
+            b = torch.empty(shape, dtype=torch.float32, device=like.device)
+            self._bufs[key] = b
+        return b
+
+    def _all_gather(self, full, loc):
+        if self.shard.world_size == 1:
+            full.copy_(loc)
+            return None
+        if not self.host_staging:
+            return dist.all_gather_into_tensor(full, loc, group=self.group, async_op=True)
+        h = torch.empty(full.shape, dtype=full.dtype)
+        dist.all_gather_into_tensor(h, loc.cpu(), group=self.group)
+        full.copy_(h)
+        return None
+
+    def _event(self, key):
+        ev = self._events.get(key)
+        if ev is None:
+            ev = self._events[key] = torch.cuda.Event()
+        return ev
+
+    def _issue(self, full, loc, key, hub_done=None):
+        """All-gather loc -> full once the work enqueued so far on the current
+        stream (and hub_done, if given) is done (GPU: from the comm stream,
+        asynchronously)."""
+        if not full.is_cuda or self.host_staging:
+            return self._all_gather(full, loc)
+        ev = self._event(("ready",) + key)
+        ev.record(torch.cuda.current_stream(full.device))
+        self._comm.wait_event(ev)
+        if hub_done is not None:
+            self._comm.wait_event(hub_done)
+        with torch.cuda.stream(self._comm):
+            return self._all_gather(full, loc)
+
+    def _split_chunk(self, csr, X, out, rows, key):
+        """Hop 1 row chunk as two launches: light rows on the current stream,
+        hub rows on the hub stream; returns the hub launch's done event."""
+        main = torch.cuda.current_stream(X.device)
+        ready, done = self._event(("in",) + key), self._event(("hub",) + key)
+        ready.record(main)
+        self.spmm_fn(csr, X, out, rows, False, "light")
+        self._hub.wait_event(ready)
+        with torch.cuda.stream(self._hub):
+            self.spmm_fn(csr, X, out, rows, False, "hub")
+        done.record(self._hub)
+        return done
+
+    def propagate(self, X0, K, out=None, output="sharded"):
+        s = self.shard
+        n, F = X0.shape
+        if n != s.n:
+            raise ValueError(f"X0 has {n} rows, S has {s.n}")
+        if output not in ("replicated", "sharded"):
+            raise ValueError(f"output must be 'replicated' or 'sharded', not {output!r}")
+        if K <= 0:
+            return X0 if output == "replicated" else X0[torch.as_tensor(self.row_index,
+                                                                       device=X0.device)]
+        Fp = F
+        if X0.is_cuda:
+            from . import _lib
+            from .propagate import aligned_ld
+            Fp = aligned_ld(F)
+            if self._comm is None:
+                self._comm = torch.cuda.Stream(device=X0.device)
+                self._hub = torch.cuda.Stream(device=X0.device)
+            pad = self.pad_input if self.pad_input is not None else s.world_size <= 4
+            if pad:
+                Xa = self._buf("x0", (n, Fp), X0)
+                _lib.check(_lib.load().sgc_pad_rows_f32(
+                    _lib.ptr(X0), X0.stride(0), _lib.ptr(Xa), Fp, n, F,
+                    _lib.stream_handle(X0.device)), "pad_rows_f32")
+                X0 = Xa
+        G, R, GR = s.groups, s.rows, s.group_rows
+        PGR = s.world_size * GR                   # exchange-buffer rows per group
+        src, works = X0, None
+        for h in range(K):
+            last = h == K - 1
+            exchanged = not last or output == "replicated"
+            if exchanged:
+                dst = self._buf(("loc", h & 1), (R, Fp), X0)
+                full = self._buf(("full", h & 1), (G * PGR, Fp), X0)
+            else:
+                if out is None:
+                    out = torch.empty((R, F), dtype=torch.float32, device=X0.device)
+                elif tuple(out.shape) != (R, F):
+                    raise ValueError(f"out must be [{R}, {F}] (local rows, padding included)")
+                dst = out
+            W = min(dst.shape[1], src.shape[1])
+            passes = [(s.csr_input, None)] if h == 0 else [(s.sub[g], g) for g in range(G)]
+            new_works = []
+            for pi, (csr, g) in enumerate(passes):
+                if g is not None and works is not None and works[g] is not None:
+                    works[g].wait()               # column group g of X_{h} has arrived
+                acc = pi > 0
+                if pi == len(passes) - 1 and exchanged:
+                    split = h == 0 and X0.is_cuda and not self.host_staging
+                    for c in range(G):            # final pass in row chunks, each sent at once
+                        rows = (c * GR, (c + 1) * GR)
+                        hub_done = None
+                        if split:
+                            hub_done = self._split_chunk(csr, src[:, :W], dst[:, :W], rows, (h, c))
+                        else:
+                            self.spmm_fn(csr, src[:, :W], dst[:, :W], rows, acc)
+                        new_works.append(self._issue(full[c * PGR:(c + 1) * PGR],
+                                                     dst[c * GR:(c + 1) * GR], (h, c), hub_done))
+                else:
+                    self.spmm_fn(csr, src[:, :W], dst[:, :W], (0, R), acc)
+            if exchanged:
+                works, src = new_works, full
+            else:
+                return dst[:s.n_valid]
+        for w in works:
+            if w is not None:
+                w.wait()
+        if out is None:
+            out = torch.empty((n, F), dtype=torch.float32, device=X0.device)
+        P, Tg, b = s.world_size, s.rounds_per_group, s.tile
+        # exchange layout (g, q, t', i) -> global order (g, t', q, i)
+        glob = src.view(G, P, Tg, b, Fp).permute(0, 2, 1, 3, 4).reshape(G * Tg * P * b, Fp)
+        out.copy_(glob[:n, :F])
+        return out
+
+
+# ---------------------------------------------------------------------------
 # 2-D partition: row blocks x feature blocks.
 
 class TiledPropagator:

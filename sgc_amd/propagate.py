@@ -59,6 +59,7 @@ SPMM_X_PADDED = 1  # sgc_spmm_csr_f32_ex flags (include/sgc_amd.h)
 SPMM_Y_PADDED = 2
 SPMM_NO_HUB = 4    # split launch: every row but the plan's hub rows
 SPMM_HUB_ONLY = 8  # split launch: only the hub rows, on the current stream
+SPMM_ACCUMULATE = 16  # column-block pass: continue the chains stored in out
 
 STATUS_ROWS_SORTED = 1
 STATUS_COLS_ASCENDING = 2
@@ -303,11 +304,14 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
     """One hop Y = S[row_begin:row_end] . X (bit-exact with torch.spmm on CPU).
     flags: SPMM_* bits of sgc_spmm_csr_f32_ex (a split launch on the GPU: NO_HUB
     / HUB_ONLY; on the CPU the whole hop runs for the NO_HUB part and nothing
-    for HUB_ONLY, so the two parts still write every row once)."""
+    for HUB_ONLY, so the two parts still write every row once; ACCUMULATE
+    continues the FMA chains already in `out`, which must then be given)."""
     X = _check_features(X, csr)
     row_end = csr.n_rows if row_end is None else row_end
     F = X.shape[1]
     if out is None:
+        if flags & SPMM_ACCUMULATE:
+            raise ValueError("sgc_amd: SPMM_ACCUMULATE continues the chains in `out`; pass it")
         out = torch.empty((row_end - row_begin, F), dtype=torch.float32, device=X.device)
     if F == 0 or row_end == row_begin:
         return out
@@ -315,10 +319,11 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
     if X.device.type == "cpu":
         if flags & SPMM_HUB_ONLY:
             return out
-        _lib.check(lib.sgc_spmm_csr_f32_cpu(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
-                                            _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
-                                            X.stride(0), _lib.ptr(out), out.stride(0), F,
-                                            cpu_threads()), "spmm_csr_f32_cpu")
+        _lib.check(lib.sgc_spmm_csr_f32_cpu_ex(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
+                                               _lib.ptr(csr.val), row_begin, row_end,
+                                               _lib.ptr(X), X.stride(0), _lib.ptr(out),
+                                               out.stride(0), F, int(flags) & ~SPMM_NO_HUB,
+                                               cpu_threads()), "spmm_csr_f32_cpu")
         return out
     pl = csr.plan(row_begin, row_end, threshold, hub_threshold, F) if use_plan else NO_PLAN
     with torch.cuda.device(X.device):

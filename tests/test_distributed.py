@@ -210,6 +210,117 @@ def test_gathered_layout():
 
 
 # ---------------------------------------------------------------------------
+# Cyclic row tiles + column-ordered exchange (CyclicRowPropagator).
+
+def test_cyclic_layout_and_split():
+    """Tiles dealt round-robin: every global row is owned once, local rows are
+    ascending, the exchange-buffer map is a bijection that sends column group
+    g to rows [g*P*Tg*b, (g+1)*P*Tg*b), and each row's group CSRs concatenate
+    to its full CSR-ordered row."""
+    from sgc_amd.distributed import cyclic_gathered_index, cyclic_layout, make_cyclic_shard
+    from oracle import oracle as o
+    rng = np.random.default_rng(3)
+    n, P, b, G = 103, 3, 4, 3
+    Tg, T = cyclic_layout(n, P, b, G)
+    assert T == G * Tg and P * T * b >= n
+    rows = rng.integers(0, n, 900)
+    cols = rng.integers(0, n, 900)
+    key = np.unique(rows * n + cols)  # canonical CSR: rows sorted by column
+    rows, cols = key // n, key % n
+    rp, ci, va = o.coo_to_csr(n, n, rows, cols, rng.standard_normal(key.size).astype(np.float32))
+    owned = []
+    for r in range(P):
+        sh = make_cyclic_shard(rp, ci, va, r, P, "cpu", tile=b, groups=G)
+        gr = sh.global_rows[:sh.n_valid]
+        assert np.all(np.diff(gr) > 0) and np.all(sh.global_rows[sh.n_valid:] >= n)
+        owned.append(gr)
+        in_rp = sh.csr_input.row_ptr.numpy()
+        for i, j in enumerate(gr):
+            full = ci[rp[j]:rp[j + 1]]
+            parts, vparts = [], []
+            for g in range(G):
+                s_rp = sh.sub[g].row_ptr.numpy()
+                k0, k1 = s_rp[i], s_rp[i + 1]
+                c = sh.sub[g].col_idx.numpy()[k0:k1]
+                lo, hi = g * P * Tg * b, (g + 1) * P * Tg * b
+                assert np.all((c >= lo) & (c < hi))
+                parts.append(c)
+                vparts.append(sh.sub[g].val.numpy()[k0:k1])
+            assert np.array_equal(np.concatenate(parts), cyclic_gathered_index(full, P, b, Tg))
+            assert np.array_equal(np.concatenate(vparts), va[rp[j]:rp[j + 1]])
+            assert np.array_equal(sh.csr_input.col_idx.numpy()[in_rp[i]:in_rp[i + 1]], full)
+    assert np.array_equal(np.sort(np.concatenate(owned)), np.arange(n))
+    m = cyclic_gathered_index(np.arange(P * T * b), P, b, Tg)
+    assert np.array_equal(np.sort(m), np.arange(P * T * b))
+
+
+def test_cyclic_rejects_rows_out_of_group_order():
+    """A storage-order row that returns to an earlier column group cannot be
+    split into ordered passes: refused loudly, fine with one group."""
+    from sgc_amd.distributed import make_cyclic_shard
+    rp = np.array([0, 3, 3, 3, 3], dtype=np.int64)
+    ci = np.array([3, 0, 1], dtype=np.int32)  # row 0: group 1, then group 0
+    va = np.ones(3, np.float32)
+    with pytest.raises(ValueError, match="column-group order"):
+        make_cyclic_shard(rp, ci, va, 0, 2, "cpu", tile=1, groups=2)
+    make_cyclic_shard(rp, ci, va, 0, 2, "cpu", tile=1, groups=1)
+
+
+def _cyclic_worker(rank, world, port, case, K, result_q, tile, groups, staging, output):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as o
+        from sgc_amd.distributed import CyclicRowPropagator
+        n = int(case["n"])
+        rp, ci, va = o.coo_to_csr(n, n, case["rows"], case["cols"], case["vals"])
+        cp = CyclicRowPropagator(rp, ci, va, rank, world, "cpu", tile=tile, groups=groups,
+                                 host_staging=staging)
+        X0 = torch.from_numpy(case["X"])
+        out = cp.propagate(X0, K, output=output)
+        out2 = cp.propagate(X0, K, output=output)  # buffers reused
+        assert torch.equal(out, out2)
+        result_q.put((rank, (out.numpy(), cp.row_index)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name,K,tile,groups,staging,output", [
+    (2, "norm_n48_F65", 2, 4, 3, False, "sharded"),
+    (3, "norm_n48_F602", 3, 2, 4, False, "replicated"),
+    (4, "hub1000_F65", 2, 16, 4, False, "sharded"),
+    (3, "hub1000_F130", 2, 8, 2, True, "sharded"),
+    (4, "raw_unsorted_dups_F7", 2, 1, 1, False, "replicated"),  # unsorted rows: one group
+    (2, "isolated_F17", 1, 4, 2, False, "replicated"),
+    (4, "norm_n48_F130", 2, 64, 1, False, "sharded")])  # one tile per rank: empty ranks
+def test_cyclic_partition_gloo_bit_exact(tiny_cases, world, name, K, tile, groups, staging,
+                                         output):
+    """Every rank's rows of X_K (column-group passes chained with
+    SPMM_ACCUMULATE through the product CPU twin) equal the reference's rows
+    bit for bit; replicated output equals all of it."""
+    case = tiny_cases[name]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cyclic_worker, args=(r, world, port, case, K, q, tile, groups,
+                                                      staging, output)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = case[f"Y{K}"]
+    seen = []
+    for r in range(world):
+        arr, ri = got[r]
+        w = want if output == "replicated" else want[ri]
+        assert arr.shape == w.shape and np.array_equal(arr.view(np.uint32), w.view(np.uint32)), r
+        seen.append(ri)
+    assert np.array_equal(np.sort(np.concatenate(seen)), np.arange(int(case["n"])))
+
+
+# ---------------------------------------------------------------------------
 # Feature (column) partition: no exchange between hops, one chunked all-gather.
 
 def test_feature_bounds():

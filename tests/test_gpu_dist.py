@@ -119,3 +119,46 @@ def test_rccl_sharded_trainer_fused_kernel(nccl_group):
     assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item())
     torch.testing.assert_close(gw.double(), Wd.grad, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(gb.double(), bd.grad, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("pad_input", [None, False])
+@pytest.mark.parametrize("output", ["replicated", "sharded"])
+@pytest.mark.parametrize("name,K,tile,groups", [("norm_n48_F602", 2, 4, 3), ("hub1000_F130", 2, 16, 4),
+                                                ("norm_n48_F65", 3, 1, 5), ("isolated_F17", 1, 8, 2),
+                                                ("norm_n48_F602", 3, 64, 1)])
+def test_cyclic_partition_world1_bit_exact(tiny_cases, oracle, name, K, tile, groups, output,
+                                           pad_input):
+    """CyclicRowPropagator on the GPU: hop >= 2 as column-group passes chained
+    by SGC_SPMM_ACCUMULATE, the last pass in row chunks each handed to the
+    exchange (a copy at world 1), the replicated output's re-ordering."""
+    from sgc_amd.distributed import CyclicRowPropagator
+    c = tiny_cases[name]
+    n = int(c["n"])
+    rp, ci, va = oracle.coo_to_csr(n, n, c["rows"], c["cols"], c["vals"])
+    cp = CyclicRowPropagator(rp, ci, va, 0, 1, "cuda", tile=tile, groups=groups,
+                             pad_input=pad_input)
+    X0 = torch.from_numpy(c["X"]).cuda()
+    out = cp.propagate(X0, K, output=output)
+    torch.cuda.synchronize()
+    want = c[f"Y{K}"] if output == "replicated" else c[f"Y{K}"][cp.row_index]
+    assert out.shape == want.shape
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    out2 = cp.propagate(X0, K, output=output)  # prepared launches replayed
+    assert torch.equal(out, out2)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("groups", [4, 8])
+def test_cyclic_partition_reddit_shape_hash(shapes_golden, groups):
+    """Full Reddit shape through the column-group passes (world 1): the
+    reference's X_2 hash."""
+    import hashlib
+    from sgc_amd import graphs
+    from sgc_amd.distributed import CyclicRowPropagator
+    g = shapes_golden["reddit"]
+    S = graphs.synthetic_graph("reddit", seed=g["seed"])
+    X = graphs.synthetic_features("reddit", g["n"], g["features"], seed=g["feature_seed"])
+    cp = CyclicRowPropagator(S.row_ptr, S.col_idx, S.val, 0, 1, "cuda", tile=64, groups=groups)
+    out = cp.propagate(torch.from_numpy(X).cuda(), 2, output="replicated")
+    torch.cuda.synchronize()
+    assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == g["outputs"]["2"]["sha"]

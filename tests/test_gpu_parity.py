@@ -319,6 +319,77 @@ def test_narrow_launches_rows_kernel(oracle, F):
         assert bits_equal(out.cpu().numpy(), want), (F, th, hub)
 
 
+def _column_split(S, bounds):
+    """S's nonzeros split by column range [bounds[g], bounds[g+1]): one CSR per
+    range over the same rows (each row's runs stay in CSR order)."""
+    rp, ci, va = (np.asarray(S.row_ptr, np.int64), np.asarray(S.col_idx),
+                  np.asarray(S.val))
+    n = rp.size - 1
+    row = np.repeat(np.arange(n), np.diff(rp))
+    grp = np.searchsorted(np.asarray(bounds), ci, side="right") - 1
+    out = []
+    for g in range(len(bounds) - 1):
+        m = grp == g
+        sub_rp = np.zeros(n + 1, np.int64)
+        np.cumsum(np.bincount(row[m], minlength=n), out=sub_rp[1:])
+        out.append((sub_rp.astype(np.int32), ci[m], va[m]))
+    return out
+
+
+@pytest.mark.parametrize("F", [602, 256, 130, 64, 36])
+@pytest.mark.parametrize("rows_per_wave", [0, 1, 2])
+@pytest.mark.parametrize("th,hub", [(40, 500), (10**9, 10**9)])
+def test_accumulate_column_block_passes(oracle, F, rows_per_wave, th, hub):
+    """SGC_SPMM_ACCUMULATE: one plain pass over column block 0 of S, then
+    accumulate passes over blocks 1, 2, ... (the cyclic multi-GPU pipeline's
+    hop) equal one pass over S bit for bit -- light, heavy and hub rows, both
+    light kernels, padded 128-B-row buffers (F = 602) and unpadded ones,
+    full and partial row ranges.  The output starts as NaN: the plain first
+    pass must write every row (zeros where block 0 has no nonzeros), and
+    accumulate passes must leave rows without nonzeros in their block as
+    they are."""
+    from sgc_amd import _lib, graphs
+    from sgc_amd.propagate import SPMM_ACCUMULATE, SPMM_X_PADDED, SPMM_Y_PADDED, DeviceCSR, spmm
+    rng = np.random.default_rng(F + rows_per_wave)
+    n = 3000
+    lo = np.concatenate([np.zeros(900, np.int64), np.full(300, 7, np.int64),
+                         rng.integers(0, n, 15000)])
+    hi = np.concatenate([np.arange(100, 1000), np.arange(1000, 1300), rng.integers(0, n, 15000)])
+    keep = lo != hi
+    a, b = np.minimum(lo, hi)[keep], np.maximum(lo, hi)[keep]
+    key = np.unique(a * n + b)
+    S = graphs.aug_norm_csr_from_pairs(n, key // n, key % n)
+    X = rng.standard_normal((n, F)).astype(np.float32)
+    want = oracle.spmm_csr(S.row_ptr, S.col_idx, S.val, X, 0, n)
+    ld = (F + 31) // 32 * 32
+    padded = F % 4 != 0 or F == 602
+    Xd = torch.zeros((n, ld if padded else F), device=DEV)[:, :F]
+    Xd.copy_(torch.from_numpy(X))
+    pad_flags = (SPMM_X_PADDED | SPMM_Y_PADDED) if padded else 0
+    lib = _lib.load()
+    _lib.check(lib.sgc_set_tuning(b"rows_per_wave", rows_per_wave), "set_tuning")
+    try:
+        for bounds in ([0, 700, 1100, 1600, n], [0, 5, n], [0, n]):
+            subs = [DeviceCSR.from_host_arrays(*t, n_cols=n) for t in _column_split(S, bounds)]
+            for r0, r1 in ((0, n), (5, 2300)):
+                out = torch.full((r1 - r0, ld if padded else F), float("nan"), device=DEV)[:, :F]
+                for g, csr in enumerate(subs):
+                    spmm(csr, Xd, r0, r1, out=out, threshold=th, hub_threshold=hub,
+                         flags=pad_flags | (SPMM_ACCUMULATE if g else 0))
+                torch.cuda.synchronize()
+                assert bits_equal(out.cpu().numpy(), want[r0:r1]), (bounds, r0, r1)
+    finally:
+        lib.sgc_set_tuning(b"rows_per_wave", 0)
+
+
+def test_accumulate_requires_out():
+    from sgc_amd.propagate import SPMM_ACCUMULATE, DeviceCSR, spmm
+    csr = DeviceCSR.from_host_arrays(np.array([0, 1], np.int32), np.array([0], np.int32),
+                                     np.ones(1, np.float32))
+    with pytest.raises(ValueError, match="ACCUMULATE"):
+        spmm(csr, torch.ones(1, 4, device=DEV), flags=SPMM_ACCUMULATE)
+
+
 def test_empty_csr_writes_zeros():
     """A CSR without a single nonzero (an empty shard: torch's empty col/val
     tensors have no storage) writes +0.0 rows, like torch.spmm."""
