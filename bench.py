@@ -14,7 +14,10 @@ work fixed, so scaling is "strong":
                 optionally pipelined in feature groups, hub rows on their own streams
   --partition tiles  R x C: row blocks x --col-blocks feature blocks; the
                 per-hop all-gather runs within each feature block's R ranks
-  --partition auto (default)  rows vs tiles, timed on the node
+  --partition cyclic  row tiles dealt round-robin; each all-gather carries one
+                column group (--cyclic-groups G) and the next hop consumes it
+                as it arrives (column-group passes, SGC_SPMM_ACCUMULATE)
+  --partition auto (default)  rows vs tiles vs cyclic, timed on the node
   --partition features  each rank runs all K hops on its block of feature
                 columns over the full S, no exchange between hops
   --output sharded (default)  each rank ends with its row block of X_K
@@ -386,6 +389,28 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
         par = (f"feature-partition x{world} ({fB}-column blocks, all K hops local) + {backend} "
                f"{exch}; output {output}")
         unit = f"rank 0's SpMM launches, {int(fb[1] - fb[0])} feature columns"
+    elif args.partition == "cyclic":
+        from sgc_amd.distributed import CyclicRowPropagator, _cyclic_spmm
+
+        def launch_bytes(csr, X, out, rows, acc=False, part="all"):
+            r0, r1 = rows
+            w = X.shape[1]
+            nz = csr.range_nnz(r0, r1)
+            return (4 * (r1 - r0 + 1) + 8 * nz + 4 * w * min(X.shape[0], nz) +
+                    4 * w * (r1 - r0) * (2 if acc else 1))
+
+        prop = CyclicRowPropagator(S.row_ptr, S.col_idx, S.val, rank, world, dev,
+                                   tile=args.cyclic_tile, groups=args.cyclic_groups,
+                                   host_staging=staging,
+                                   spmm_fn=bracket(_cyclic_spmm, launch_bytes))
+        sh = prop.shard
+        exch = ("all-gathers of X_k after each hop but the last" if output == "sharded" else
+                "all-gathers of X_k after every hop")
+        par = (f"cyclic row tiles x{world} ({sh.tile}-row tiles round-robin) + {backend} {exch}, "
+               f"{sh.groups} per hop, each one column group, consumed as it arrives by "
+               f"column-group passes (SGC_SPMM_ACCUMULATE); output {output}")
+        unit = (f"rank 0's SpMM launches ({sh.n_valid} rows, {sh.nnz} nnz, "
+                f"{sh.groups} row chunks / column-group passes per hop)")
     else:
         from sgc_amd.distributed import (RowPartitionedPropagator, TiledPropagator,
                                          _default_spmm, feature_bounds, make_shard)
@@ -459,10 +484,16 @@ def main():
                     help="gloo = host-staged rehearsal of the N>1 path (ranks may share a GPU)")
     ap.add_argument("--distributed-path", action="store_true",
                     help="run the N>1 path even at N=1 (exercises RCCL on one GPU)")
-    ap.add_argument("--partition", default="auto", choices=["auto", "rows", "tiles", "features"],
+    ap.add_argument("--partition", default="auto",
+                    choices=["auto", "rows", "tiles", "cyclic", "features"],
                     help="N>1: split the rows of S (per-hop all-gather), rows x feature blocks "
-                         "(tiles, --col-blocks), the feature columns, or auto = rows vs tiles "
-                         "timed on the node")
+                         "(tiles, --col-blocks), round-robin row tiles with column-ordered "
+                         "exchange (cyclic), the feature columns, or auto = rows vs tiles vs "
+                         "cyclic timed on the node")
+    ap.add_argument("--cyclic-groups", type=int, default=3,
+                    help="N>1 cyclic: column groups (= all-gathers) per hop")
+    ap.add_argument("--cyclic-tile", type=int, default=64,
+                    help="N>1 cyclic: rows per round-robin tile")
     ap.add_argument("--col-blocks", type=int, default=2,
                     help="N>1 tiles: feature blocks C (P = R x C)")
     ap.add_argument("--output", default="sharded", choices=["sharded", "replicated"],
@@ -546,7 +577,7 @@ def main():
         # row partition vs 2-D tiles: timed on this node (max over ranks), so
         # the exchange rate the node actually has decides, not an estimate
         import copy
-        cands = ["rows"]
+        cands = ["rows", "cyclic"]
         if world >= 4 and world % args.col_blocks == 0 and args.output == "sharded":
             cands.append("tiles")
         trials = {}

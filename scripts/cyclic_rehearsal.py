@@ -71,27 +71,36 @@ def launch_plan(K, G, output="sharded"):
     return plan
 
 
-def durations(plan, light, hub):
-    """(main-stream ms, hub-stream ms) per plan entry from the timing records:
-    hop 1's chunks are split launches (a light record with no hub kernel, then
-    a hub-only record -- empty light interval -- when the chunk has hub rows);
-    every other launch is one record whose hub kernel is joined, so its
-    duration is the longer of the two."""
+def durations(plan, light, hub, has_hub):
+    """(main-stream ms, hub-stream ms) per plan entry from the timing records.
+    Hop 1's chunks are split launches: first the hub-only launches of all
+    chunks (a record each, empty light interval, hub time set -- none for a
+    chunk without hub rows), then the light launches (hub None).  Every other
+    launch is one record whose hub kernel is joined, so its duration is the
+    longer of the two."""
     recs = list(zip(light, hub))
     out, i = [], 0
+    n0 = sum(1 for p in plan if p[0] == 0 and p[1] == "chunk")
+    hubs = []
+    while i < len(recs) and len(hubs) < n0 and recs[i][1] is not None and recs[i][0] < 0.02:
+        hubs.append(recs[i][1])
+        i += 1
     for h, kind, idx, g in plan:
         lt, hb = recs[i]
         i += 1
         if h == 0 and kind == "chunk":
-            hub_ms = 0.0
-            if i < len(recs) and recs[i][1] is not None and recs[i][0] < 1e-3:
-                hub_ms = recs[i][1]
-                i += 1
-            out.append((lt, hub_ms))
+            out.append((lt, 0.0))
         else:
             out.append((max(lt, hb or 0.0), 0.0))
+    # the hub-only launches run back to back on the hub stream from the start
+    # of hop 1; chunks without hub rows (has_hub False) have no record
+    owners = [c for c in range(n0) if has_hub[c]]
+    if len(owners) != len(hubs):
+        raise RuntimeError(f"{len(hubs)} hub records for {len(owners)} chunks with hub rows")
+    for c, hb in zip(owners, hubs):
+        out[c] = (out[c][0], hb)
     if i != len(recs):
-        raise RuntimeError(f"{len(recs)} timing records, {i} matched to the launch plan")
+        raise RuntimeError(f"{len(recs)} timing records, {i} matched to the launch plan: {recs}")
     return out
 
 
@@ -110,7 +119,7 @@ def simulate(plan, dur, G, bytes_per_gather, P, bw_gbs):
         if g is not None and kind == "chunk":  # final pass g = G-1 needs gather G-1
             start = max(start, arrive_prev[G - 1])
         d_main, d_hub = dur[i]
-        hub_t = max(hub_t, start) + d_hub
+        hub_t = hub_t + d_hub  # hop-1 hub launches: back to back from t = 0
         main = start + d_main
         if kind == "chunk":
             t = (P - 1) / P * bytes_per_gather / (bw_gbs * 1e9) * 1e3
@@ -128,7 +137,14 @@ def main():
     ap.add_argument("--bw", default="300,450,600", help="assumed all-gather ingress GB/s per rank")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks to time")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="sgc_set_tuning knob (applies to every launch, single-GPU step included)")
     args = ap.parse_args()
+    if args.tune:
+        from sgc_amd import _lib
+        for kv in args.tune:
+            k, v = kv.split("=", 1)
+            _lib.check(_lib.load().sgc_set_tuning(k.encode(), int(v)), f"set_tuning {kv}")
     spec = graphs.SHAPES[args.shape]
     S = graphs.synthetic_graph(args.shape, seed=0)
     F, K, n = spec["features"], spec["hops"], S.n
@@ -138,7 +154,8 @@ def main():
     out = torch.empty((n, F), device="cuda")
     t1 = timeit(lambda: propagate(csr, X0, K, out=out), args.reps)
     del csr
-    print(json.dumps({"case": "single", "shape": args.shape, "ms": t1 * 1e3}), flush=True)
+    print(json.dumps({"case": "single", "shape": args.shape, "ms": t1 * 1e3, "tune": args.tune}),
+          flush=True)
     bws = [float(b) for b in args.bw.split(",")]
     for P in (int(x) for x in args.P.split(",")):
         for tile in (int(x) for x in args.tiles.split(",")):
@@ -157,7 +174,11 @@ def main():
                     kernel_timing(False)
                     light, hub = collect_kernel_timing()
                     plan = launch_plan(K, G)
-                    dur = durations(plan, light, hub)
+                    ci = sh.csr_input
+                    has_hub = [ci.plan(c * sh.group_rows, (c + 1) * sh.group_rows,
+                                       width=Fp if P <= 4 else F).n_hub > 0  # hop-1 width
+                               for c in range(G)]
+                    dur = durations(plan, light, hub, has_hub)
                     gbytes = P * sh.group_rows * Fp * 4
                     free = simulate(plan, dur, G, gbytes, P, 1e12)
                     proj = {f"{bw:g}GBps": t * 1e3 + simulate(plan, dur, G, gbytes, P, bw) - free

@@ -1,36 +1,33 @@
-"""K-hop propagation across GPUs (one process per GPU): two partitions, two
+"""K-hop propagation across GPUs (one process per GPU): four partitions, two
 output layouts, and the data-parallel classifier that consumes them.
 
-RowPartitionedPropagator (the north star's layout, the
-default of bench.py --gpus N): each output row of S.X is an independent FMA chain, so the
-hot path shards by 1-D row slicing of S.  Rank p owns rows [r_p, r_{p+1}),
-chosen by equal nonzero count (prefix of row_ptr) so power-law hubs do not
-unbalance the ranks, and computes those rows of X_{k+1} with the same HIP
-kernel (sgc_spmm_csr_f32 over a row range, global column indices).  Between
-hops every rank needs all of X_k (at Reddit/RMAT shape nearly every column is
-referenced by every row block), so the exchange is one all-gather of the row
-blocks per hop -- RCCL over xGMI with the "nccl" backend (gloo in the CPU
-tests).  Blocks are equal row ranges of B = ceil(N/P) rows (the last one
-shorter), so all_gather_into_tensor lands row j of X_k at row j of the
-gathered [P*B, Fg] buffer: the next hop reads it with the original column
-indices, and no padding crosses xGMI except the last block's tail.  (Equal
-rows rather than equal nonzeros: the exchange, not the SpMM, bounds the hop at
-large P, and on the randomly labelled Reddit-shape graph equal rows leave the
-nonzeros within 5% of balanced at P=8; nnz_balanced_bounds is kept for
-graphs where they are not.)
+RowPartitionedPropagator (the north star's layout): each
+output row of S.X is an independent FMA chain, so the hot path shards by 1-D
+row slicing of S.  Rank p owns the contiguous rows [r_p, r_{p+1}), chosen by
+equal nonzero count so power-law hubs do not unbalance the ranks, and
+computes those rows of X_{k+1} with the HIP kernel.  Between hops every rank
+needs all of X_k (at Reddit/RMAT shape nearly every column is referenced by
+every row block), so the exchange is an all-gather of the row blocks per hop
+-- RCCL over xGMI with the "nccl" backend (gloo in the CPU tests) -- into a
+[P*B, F] buffer (B = the largest block; the rank's CSR carries a second
+column-index array in that layout).  Pipelines: one full-width group, feature
+groups (group g's all-gather overlaps group g+1's compute), or row chunks
+(chunk c all-gathered as soon as it is computed); autotune() picks on the node.
 
-Overlap: features are processed in groups (independent FMA chains, so any
-grouping is bit-exact).  Each group's local SpMM is followed by that group's
-asynchronous all-gather, so RCCL moves group g while the SpMM computes group
-g+1, and the next hop waits only for its own group.
+CyclicRowPropagator: row tiles dealt round-robin, so all-gather g of X_k
+delivers column group g and hop k+1 consumes it as it arrives (column-group
+passes chained by SGC_SPMM_ACCUMULATE, bit-identical to one pass).
+
+TiledPropagator: P = R x C, row blocks x feature blocks (each feature block a
+row partition over its R ranks).
 
 FeaturePartitionedPropagator: S.X acts on each feature column independently,
 so rank p owns a block of feature columns and runs all K hops over the full S
 with no exchange between hops (see its docstring for the measured trade-off).
 
 Output: "replicated" (every rank gets all of X_K) or "sharded" (every rank
-keeps its equal-row block of X_K, which is what ShardedSGCTrainer -- the
-data-parallel SGC classifier -- consumes; no full X_K is ever materialised).
+keeps its rows of X_K, which is what ShardedSGCTrainer -- the data-parallel
+SGC classifier -- consumes; no full X_K is ever materialised).
 """
 from dataclasses import dataclass
 from typing import Callable, Optional
@@ -734,10 +731,12 @@ class CyclicRowPropagator:
     computes out[rows] (default: the HIP engine on ROCm tensors, the CPU twin
     on CPU tensors).
 
-    Hub rows: hop 1's row chunks run as split launches (every row but the hub
-    rows on the compute stream, the hub rows on a hub stream; all-gather c
-    waits for both), so a 0.3-ms hub chain in chunk c does not hold back chunk
-    c+1.  The column-group passes keep each launch's hub kernel joined: a row
+    Hub rows: hop 1's row chunks run as split launches -- the hub rows of
+    every chunk first, on a hub stream, then the light rows chunk by chunk on
+    the compute stream; all-gather c waits for both halves of chunk c -- so a
+    0.3-ms hub chain does not hold back the next chunk, and the hub
+    workgroups (a CU's LDS each) are not starved by light chunks issued
+    before them.  The column-group passes keep each launch's hub kernel joined: a row
     that is a hub of pass g may be a light row of pass g+1, which must not
     start on it before pass g's chain has stored."""
 
@@ -797,17 +796,22 @@ class CyclicRowPropagator:
         with torch.cuda.stream(self._comm):
             return self._all_gather(full, loc)
 
-    def _split_chunk(self, csr, X, out, rows, key):
-        """Hop 1 row chunk as two launches: light rows on the current stream,
-        hub rows on the hub stream; returns the hub launch's done event."""
+    def _hub_first(self, csr, X, out, chunks, h):
+        """Hop 1's hub rows, issued before any of its light chunks: one
+        HUB_ONLY launch per row chunk on the hub stream (after the work already
+        on the current stream), so their CU-sized workgroups are placed before
+        the light chunks fill the machine.  Returns each chunk's done event."""
         main = torch.cuda.current_stream(X.device)
-        ready, done = self._event(("in",) + key), self._event(("hub",) + key)
+        ready = self._event(("in", h))
         ready.record(main)
-        self.spmm_fn(csr, X, out, rows, False, "light")
         self._hub.wait_event(ready)
+        done = []
         with torch.cuda.stream(self._hub):
-            self.spmm_fn(csr, X, out, rows, False, "hub")
-        done.record(self._hub)
+            for c, rows in enumerate(chunks):
+                self.spmm_fn(csr, X, out, rows, False, "hub")
+                ev = self._event(("hub", h, c))
+                ev.record(self._hub)
+                done.append(ev)
         return done
 
     def propagate(self, X0, K, out=None, output="sharded"):
@@ -858,16 +862,15 @@ class CyclicRowPropagator:
                     works[g].wait()               # column group g of X_{h} has arrived
                 acc = pi > 0
                 if pi == len(passes) - 1 and exchanged:
+                    chunks = [(c * GR, (c + 1) * GR) for c in range(G)]
                     split = h == 0 and X0.is_cuda and not self.host_staging
-                    for c in range(G):            # final pass in row chunks, each sent at once
-                        rows = (c * GR, (c + 1) * GR)
-                        hub_done = None
-                        if split:
-                            hub_done = self._split_chunk(csr, src[:, :W], dst[:, :W], rows, (h, c))
-                        else:
-                            self.spmm_fn(csr, src[:, :W], dst[:, :W], rows, acc)
+                    hub_done = (self._hub_first(csr, src[:, :W], dst[:, :W], chunks, h) if split
+                                else [None] * G)
+                    for c, rows in enumerate(chunks):  # final pass in row chunks, each sent at once
+                        self.spmm_fn(csr, src[:, :W], dst[:, :W], rows, acc,
+                                     "light" if split else "all")
                         new_works.append(self._issue(full[c * PGR:(c + 1) * PGR],
-                                                     dst[c * GR:(c + 1) * GR], (h, c), hub_done))
+                                                     dst[c * GR:(c + 1) * GR], (h, c), hub_done[c]))
                 else:
                     self.spmm_fn(csr, src[:, :W], dst[:, :W], (0, R), acc)
             if exchanged:
