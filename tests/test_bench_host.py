@@ -1,0 +1,50 @@
+"""bench.py's host-side accounting (no GPU): the byte models of SURVEY.md
+8(d), the measured-traffic roofline and its refusal of a PMC record taken on
+a different library build, and the host-core count the CPU baseline reports."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+REDDIT = dict(n=232965, nnz=23446803, F=602)
+
+
+def test_byte_models_reddit():
+    # the figures DESIGN.md 5 quotes per hop at the Reddit shape
+    assert bench.gather_model_bytes(**REDDIT) == 57209387632
+    assert bench.compulsory_bytes(**REDDIT) == 1310465728
+
+
+def test_roofline_refuses_traffic_of_another_build():
+    rec = bench.roofline("reddit", REDDIT["n"], REDDIT["nnz"], REDDIT["F"], 4.65, 4.45, 4.6,
+                         "0" * 64, "one hop")
+    assert rec["traffic"] is None and "refused" in rec["traffic_source"]
+    assert rec["frac"] == pytest.approx(rec["compulsory_frac"])
+    assert rec["hub_tail_ms"] == pytest.approx(0.15)
+
+
+@pytest.mark.parametrize("shape", ["reddit", "rmat"])
+def test_roofline_uses_matching_pmc_record(shape):
+    path = os.path.join(ROOT, "profiles", f"pmc_{shape}.json")
+    pmc = json.load(open(path))
+    pmc_sha = pmc["lib_sha256"]
+    traffic, src = bench.load_traffic(shape, pmc_sha)
+    assert traffic is not None and traffic["hbm_bytes_per_launch"] > 0
+    ms = float(pmc["kernel_ms"])  # the hop time the counters were taken over
+    rec = bench.roofline(shape, REDDIT["n"], REDDIT["nnz"], REDDIT["F"], ms, ms, None,
+                         pmc_sha, "one hop")
+    t = ms * 1e-3
+    assert rec["traffic"] == traffic["hbm_bytes_per_launch"]
+    assert rec["frac"] == pytest.approx(rec["traffic"] / t / 1e9 / bench.HBM_PEAK_GBS)
+    assert 0 < rec["frac"] <= 1.0
+
+
+def test_host_cores_positive():
+    n, how = bench.host_cores()
+    assert n >= 1 and "sched_getaffinity" in how
