@@ -55,9 +55,14 @@ const char *sgc_last_error(void);
  *   "hub_priority": 1 = hub kernel on a highest-priority stream (default 0);
  *   "hub_first":    1 = hub kernel on the caller's stream, the light/heavy
  *                   kernel on the side stream (default 0: the reverse);
+ *   "hub_stream":   1 = hub kernel on a side stream, concurrent with the
+ *                   light kernel; 2 = on the caller's stream before the light
+ *                   kernel (serial, no cross-stream events); 0 = default: the
+ *                   side stream unless the launch sets SGC_SPMM_HUB_SERIAL;
  *   "rows_per_wave": light rows per wavefront when 16-B lanes are possible
- *                   (2 = default: 32 lanes x 4 floats per row; 4; 1 = one row
- *                   per wave with the slice_floats / max_vec scheme).
+ *                   (0 = default, auto; 2 = 32 lanes x 4 floats per row; 4 =
+ *                   16 lanes; 1 = one row per wave with the slice_floats /
+ *                   max_vec scheme).
  * sgc_get_tuning returns -1 for an unknown key. */
 int sgc_set_tuning(const char *key, int64_t value);
 int64_t sgc_get_tuning(const char *key);
@@ -213,9 +218,13 @@ int sgc_timing_collect(float *light_ms_host, float *hub_ms_host, int64_t capacit
  * nonzeros of S_g precede those of S_{g+1} in CSR order), one unflagged
  * launch over S_0 followed by ACCUMULATE launches over S_1, S_2, ... writes
  * exactly what one launch over S writes (the fp32 store/load between passes
- * is exact). */
+ * is exact).
+ * SGC_SPMM_HUB_SERIAL: run the hub rows' kernel on `stream` before the light
+ * kernel instead of beside it on a side stream (no fork/join events); for
+ * launches whose longest hub chain is shorter than the ~20-30 us a
+ * cross-stream fork/join costs (sgc_set_tuning "hub_stream" overrides). */
 enum { SGC_SPMM_X_PADDED = 1, SGC_SPMM_Y_PADDED = 2, SGC_SPMM_NO_HUB = 4,
-       SGC_SPMM_HUB_ONLY = 8, SGC_SPMM_ACCUMULATE = 16 };
+       SGC_SPMM_HUB_ONLY = 8, SGC_SPMM_ACCUMULATE = 16, SGC_SPMM_HUB_SERIAL = 32 };
 int sgc_spmm_csr_f32_ex(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                         int64_t row_begin, int64_t row_end,
                         const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,

@@ -1058,6 +1058,14 @@ static int g_hub_chunk = 0;
 // kernel on the caller's stream, light/heavy kernel on the side stream (the
 // hub workgroups are placed first).  Set through sgc_set_tuning("hub_first").
 static int g_hub_first = 0;
+// Where the hub kernel runs: 1 = a side stream, concurrent with the light
+// kernel (fork + join events: ~20-30 us of cross-queue synchronisation per
+// launch); 2 = the caller's stream, before the light kernel (serial: costs
+// the hub kernel's own time); 0 = per launch, serial when the caller sets
+// SGC_SPMM_HUB_SERIAL (the Python layer does when the longest hub chain is
+// shorter than that synchronisation: Pubmed shape 70 -> 61 us per hop).
+// Set through sgc_set_tuning("hub_stream").
+static int g_hub_stream = 0;
 
 int set_tuning(const char *key, int64_t value) {
     SGC_REQUIRE(key, SGC_EINVAL, "set_tuning: null key");
@@ -1080,6 +1088,11 @@ int set_tuning(const char *key, int64_t value) {
     if (std::string(key) == "hub_first") {
         SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "hub_first must be 0 or 1");
         g_hub_first = (int)value;
+        return SGC_OK;
+    }
+    if (std::string(key) == "hub_stream") {
+        SGC_REQUIRE(value >= 0 && value <= 2, SGC_EINVAL, "hub_stream must be 0, 1 or 2");
+        g_hub_stream = (int)value;
         return SGC_OK;
     }
     if (std::string(key) == "rows_per_wave") {
@@ -1110,6 +1123,7 @@ int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
     if (key && std::string(key) == "hub_priority") return g_hub_priority;
     if (key && std::string(key) == "hub_first") return g_hub_first;
+    if (key && std::string(key) == "hub_stream") return g_hub_stream;
     return -1;
 }
 
@@ -1158,7 +1172,9 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         const int n_chunks = (int)((F + hc - 1) / hc);
         SGC_REQUIRE(n_hub * n_chunks < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many hub items");
         hipStream_t hs = stream;  // HUB_ONLY: on the caller's stream, nothing else
-        if (!hub_only) {
+        const bool serial =
+            g_hub_stream == 2 || (g_hub_stream == 0 && (flags & SGC_SPMM_HUB_SERIAL));
+        if (!hub_only && !serial) {
             SGC_HIP_CHECK(side_stream(&side));
             side_lock = std::unique_lock<std::mutex>(side->mu);
             SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
@@ -1204,7 +1220,14 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     const bool v4_ok = ldx % 4 == 0 && xa % 16 == 0 && F4 <= ldx && F4 >= 32 &&
                        (F4 == F || (flags & SGC_SPMM_X_PADDED));
     const bool csr_v4 = F % 4 == 0 && pick_vec(F, ldx, ldy, X, Y) == 4;
-    const bool rows_kernel = v4_ok && g_rows_per_wave != 1 &&
+    // Small, wide launches (Cora shape: 2,708 rows x 1,433 features, X in
+    // L2): latency-bound, so fewer and wider work items win -- the one-row
+    // kernel with 512-float slices, 19.7 vs 24.9 us per hop for the
+    // 128-float rows kernel (profiles/r02/small_shapes_sweep.log).  Only at
+    // the default schedule knobs.
+    const bool small_wide = n_rows * F <= (int64_t(1) << 23) && F > 256 &&
+                            g_rows_per_wave == 0 && g_slice_floats == 128;
+    const bool rows_kernel = v4_ok && g_rows_per_wave != 1 && !small_wide &&
                              (g_rows_per_wave > 1 || !csr_v4 || F4 < 128);
     hipError_t e = hipSuccess;
     if (rows_kernel) {
@@ -1235,7 +1258,8 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         const int V = pick_vec(F, ldx, ldy, X, Y);
         const int chunks_total = (int)((F + kWave * V - 1) / (kWave * V));
         const int cmax = max_chunks(V);
-        int C = g_slice_floats > 0 ? std::max(1, g_slice_floats / (kWave * V)) : cmax;
+        const int sf = small_wide ? 512 : g_slice_floats;
+        int C = sf > 0 ? std::max(1, sf / (kWave * V)) : cmax;
         C = std::min(C, std::min(cmax, chunks_total));
         const int slices = (chunks_total + C - 1) / C;
         const int64_t waves = n_heavy * (int64_t)C * V + n_rows;  // upper bound (VH >= 1)

@@ -51,6 +51,11 @@ class Plan(NamedTuple):
     n_heavy: int
     n_hub: int
     threshold: int
+    max_hub_degree: int = 0  # nonzeros of the longest hub row (0: no hub rows)
+
+    def hub_flags(self):
+        """SPMM_HUB_SERIAL when the hub kernel is short enough to run in line."""
+        return SPMM_HUB_SERIAL if 0 < self.max_hub_degree <= HUB_SERIAL_MAX_DEGREE else 0
 
 
 NO_PLAN = Plan(None, 0, 0, 0)
@@ -60,6 +65,11 @@ SPMM_Y_PADDED = 2
 SPMM_NO_HUB = 4    # split launch: every row but the plan's hub rows
 SPMM_HUB_ONLY = 8  # split launch: only the hub rows, on the current stream
 SPMM_ACCUMULATE = 16  # column-block pass: continue the chains stored in out
+SPMM_HUB_SERIAL = 32  # hub kernel before the light kernel on the same stream
+# Longest hub row (nonzeros) for which the serial hub launch beats the
+# side-stream fork/join: its chain (~6.4 ns per nonzero) plus a
+# launch stays under the ~25 us the two cross-stream events cost.
+HUB_SERIAL_MAX_DEGREE = 3072
 
 STATUS_ROWS_SORTED = 1
 STATUS_COLS_ASCENDING = 2
@@ -240,8 +250,13 @@ class DeviceCSR:
                                               hub, _lib.ptr(buf), cap, ctypes_byref(n_heavy),
                                               ctypes_byref(n_hub),
                                               _lib.stream_handle(self.device)), "plan_build")
-            h = int(n_heavy.value)
-            self._plans[key] = Plan(buf[:max(h, 1)].clone(), h, int(n_hub.value), threshold)
+            h, nh = int(n_heavy.value), int(n_hub.value)
+            deg = 0
+            if nh > 0:  # heaviest first: row 0 of the plan is the longest hub chain
+                r = int(buf[0].item())
+                ends = self.row_ptr[[r, r + 1]].tolist()
+                deg = ends[1] - ends[0]
+            self._plans[key] = Plan(buf[:max(h, 1)].clone(), h, nh, threshold, deg)
         return self._plans[key]
 
 
@@ -331,7 +346,8 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
                                            _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
                                            X.stride(0), _lib.ptr(out), out.stride(0), F,
                                            _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
-                                           int(flags), _lib.stream_handle(X.device)),
+                                           int(flags) | pl.hub_flags(),
+                                           _lib.stream_handle(X.device)),
                    "spmm_csr_f32")
     return out
 
@@ -359,7 +375,7 @@ class SpmmLaunch:
         self._args = (_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val),
                       int(row_begin), int(row_end), _lib.ptr(X), X.stride(0), _lib.ptr(out),
                       out.stride(0), F, _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
-                      int(flags))
+                      int(flags) | pl.hub_flags())
 
     def __call__(self, stream_handle):
         rc = self._fn(*self._args, stream_handle)
@@ -445,7 +461,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
             dst = out if h == K - 1 else bufs[nxt][:, :F]
             # the engine's own buffers may be read / written in their pad columns
             flags = ((SPMM_X_PADDED if src is not X else 0) |
-                     (SPMM_Y_PADDED if dst is not out else 0))
+                     (SPMM_Y_PADDED if dst is not out else 0) | pl.hub_flags())
             if hop_hook:
                 hop_hook("start", h)
             _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),

@@ -382,6 +382,31 @@ def test_accumulate_column_block_passes(oracle, F, rows_per_wave, th, hub):
         lib.sgc_set_tuning(b"rows_per_wave", 0)
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_hub_stream_modes_bit_exact(tiny_cases, oracle, mode):
+    """Hub kernel beside the light kernel (side stream, fork/join), in line
+    before it (SGC_SPMM_HUB_SERIAL / hub_stream=2) or per the plan's longest
+    hub row (default): the same bits."""
+    from sgc_amd import _lib
+    from sgc_amd.propagate import DeviceCSR, HUB_SERIAL_MAX_DEGREE, propagate
+    lib = _lib.load()
+    _lib.check(lib.sgc_set_tuning(b"hub_stream", mode), "set_tuning")
+    try:
+        for name in ("hub1000_F130", "hub1000_F65", "norm_n48_F602"):
+            c = tiny_cases[name]
+            n = int(c["n"])
+            rp, ci, va = oracle.coo_to_csr(n, n, c["rows"], c["cols"], c["vals"])
+            csr = DeviceCSR.from_host_arrays(rp, ci, va)
+            pl = csr.plan(0, n, 7, 7, c["X"].shape[1])
+            if name.startswith("hub"):
+                assert 0 < pl.max_hub_degree <= HUB_SERIAL_MAX_DEGREE
+            out = propagate(csr, torch.from_numpy(c["X"]).to(DEV), 2, threshold=7, hub_threshold=7)
+            torch.cuda.synchronize()
+            assert bits_equal(out.cpu().numpy(), c["Y2"]), (name, mode)
+    finally:
+        lib.sgc_set_tuning(b"hub_stream", 0)
+
+
 def test_accumulate_requires_out():
     from sgc_amd.propagate import SPMM_ACCUMULATE, DeviceCSR, spmm
     csr = DeviceCSR.from_host_arrays(np.array([0, 1], np.int32), np.array([0], np.int32),
