@@ -392,7 +392,7 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
     elif args.partition == "cyclic":
         from sgc_amd.distributed import CyclicRowPropagator, _cyclic_spmm
 
-        def launch_bytes(csr, X, out, rows, acc=False, part="all"):
+        def launch_bytes(csr, X, out, rows, acc=False, part="all", thresholds=None):
             r0, r1 = rows
             w = X.shape[1]
             nz = csr.range_nnz(r0, r1)

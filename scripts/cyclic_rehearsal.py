@@ -175,8 +175,9 @@ def main():
                     light, hub = collect_kernel_timing()
                     plan = launch_plan(K, G)
                     ci = sh.csr_input
-                    has_hub = [ci.plan(c * sh.group_rows, (c + 1) * sh.group_rows,
-                                       width=Fp if P <= 4 else F).n_hub > 0  # hop-1 width
+                    th, hb = cp._th  # the rank-level thresholds every launch used
+                    has_hub = [ci.plan(c * sh.group_rows, (c + 1) * sh.group_rows, th, hb,
+                                       Fp if P <= 4 else F).n_hub > 0  # hop-1 width
                                for c in range(G)]
                     dur = durations(plan, light, hub, has_hub)
                     gbytes = P * sh.group_rows * Fp * 4

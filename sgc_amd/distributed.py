@@ -662,20 +662,22 @@ def _pad_columns_allocated(t):
     return end * t.element_size() <= t.untyped_storage().nbytes()
 
 
-def _cyclic_spmm(csr, X, out, rows, accumulate, part="all"):
+def _cyclic_spmm(csr, X, out, rows, accumulate, part="all", thresholds=(None, None)):
     """Rows [r0, r1) of csr . X into out[r0:r1] through the product engine;
     accumulate = continue the chains stored in out (SPMM_ACCUMULATE); part =
-    "all", or the split launch "light" (all but the hub rows) / "hub"."""
+    "all", or the split launch "light" (all but the hub rows) / "hub";
+    thresholds = (heavy, hub) row-length thresholds of the plan."""
     from . import _lib
     from .propagate import (SPMM_ACCUMULATE, SPMM_HUB_ONLY, SPMM_NO_HUB, SPMM_X_PADDED,
                             SPMM_Y_PADDED, SpmmLaunch, spmm)
     r0, r1 = rows
+    th, hub = thresholds
     flags = (SPMM_ACCUMULATE if accumulate else 0) | \
         {"all": 0, "light": SPMM_NO_HUB, "hub": SPMM_HUB_ONLY}[part]
     if X.shape[1] < out.shape[1]:
         raise ValueError("output wider than input")
     if not X.is_cuda:
-        return spmm(csr, X, r0, r1, out=out[r0:r1], flags=flags)
+        return spmm(csr, X, r0, r1, out=out[r0:r1], flags=flags, threshold=th, hub_threshold=hub)
     # the engine's own buffers have 128-B rows: let the kernel use 16-B lanes
     # (columns [F, round4(F)) of every row allocated; their values unused)
     if _pad_columns_allocated(X):
@@ -683,13 +685,14 @@ def _cyclic_spmm(csr, X, out, rows, accumulate, part="all"):
     if _pad_columns_allocated(out):
         flags |= SPMM_Y_PADDED
     launches = csr.__dict__.setdefault("_launches", {})
-    key = (r0, r1, flags, X.data_ptr(), tuple(X.shape), X.stride(0), out.data_ptr(),
+    key = (r0, r1, flags, th, hub, X.data_ptr(), tuple(X.shape), X.stride(0), out.data_ptr(),
            tuple(out.shape), out.stride(0))
     fn = launches.get(key)
     if fn is None:
         if len(launches) > 256:
             launches.clear()
-        fn = launches[key] = SpmmLaunch(csr, X, out[r0:r1], r0, r1, flags)
+        fn = launches[key] = SpmmLaunch(csr, X, out[r0:r1], r0, r1, flags, threshold=th,
+                                        hub_threshold=hub)
     fn(_lib.stream_handle(X.device))
     return out
 
@@ -727,9 +730,15 @@ class CyclicRowPropagator:
 
     output="sharded": this rank's rows of X_K, in ascending global order,
     global ids in `row_index` (valid rows only).  output="replicated": X_K
-    [N, F] on every rank.  spmm_fn(csr, X, out, rows, accumulate, part)
-    computes out[rows] (default: the HIP engine on ROCm tensors, the CPU twin
+    [N, F] on every rank.  spmm_fn(csr, X, out, rows, accumulate, part,
+    thresholds) computes out[rows] (default: the HIP engine on ROCm tensors, the CPU twin
     on CPU tensors).
+
+    Heavy/hub row thresholds come from the rank's whole CSR (its nonzeros and
+    the width), not from each chunk or pass: sized per chunk, the hub
+    threshold (nnz / 1024) would fall to ~1k nonzeros at P = 8 and turn
+    thousands of mid-size rows into CU-sized hub workgroups (hop 1's hub
+    launches then ran 1.1-1.8 ms beside 0.6 ms of light rows).
 
     Hub rows: hop 1's row chunks run as split launches -- the hub rows of
     every chunk first, on a hub stream, then the light rows chunk by chunk on
@@ -753,6 +762,7 @@ class CyclicRowPropagator:
         self._comm = None
         self._hub = None
         self._events = {}
+        self._th = (None, None)
 
     @property
     def row_index(self):
@@ -796,6 +806,18 @@ class CyclicRowPropagator:
         with torch.cuda.stream(self._comm):
             return self._all_gather(full, loc)
 
+    def _thresholds(self, F):
+        """(heavy, hub) thresholds for every launch of this rank at width F."""
+        from .propagate import (DEFAULT_HEAVY_THRESHOLD, DEFAULT_HUB_THRESHOLD,
+                                auto_heavy_threshold, auto_hub_threshold)
+        th = DEFAULT_HEAVY_THRESHOLD
+        if th is None:
+            th = auto_heavy_threshold(self.shard.nnz, F)
+        hub = DEFAULT_HUB_THRESHOLD
+        if hub is None:
+            hub = auto_hub_threshold(self.shard.nnz, th)
+        return int(th), int(max(hub, th))
+
     def _hub_first(self, csr, X, out, chunks, h):
         """Hop 1's hub rows, issued before any of its light chunks: one
         HUB_ONLY launch per row chunk on the hub stream (after the work already
@@ -808,7 +830,7 @@ class CyclicRowPropagator:
         done = []
         with torch.cuda.stream(self._hub):
             for c, rows in enumerate(chunks):
-                self.spmm_fn(csr, X, out, rows, False, "hub")
+                self.spmm_fn(csr, X, out, rows, False, "hub", self._th)
                 ev = self._event(("hub", h, c))
                 ev.record(self._hub)
                 done.append(ev)
@@ -841,6 +863,7 @@ class CyclicRowPropagator:
                 X0 = Xa
         G, R, GR = s.groups, s.rows, s.group_rows
         PGR = s.world_size * GR                   # exchange-buffer rows per group
+        self._th = self._thresholds(F)
         src, works = X0, None
         for h in range(K):
             last = h == K - 1
@@ -868,11 +891,11 @@ class CyclicRowPropagator:
                                 else [None] * G)
                     for c, rows in enumerate(chunks):  # final pass in row chunks, each sent at once
                         self.spmm_fn(csr, src[:, :W], dst[:, :W], rows, acc,
-                                     "light" if split else "all")
+                                     "light" if split else "all", self._th)
                         new_works.append(self._issue(full[c * PGR:(c + 1) * PGR],
                                                      dst[c * GR:(c + 1) * GR], (h, c), hub_done[c]))
                 else:
-                    self.spmm_fn(csr, src[:, :W], dst[:, :W], (0, R), acc)
+                    self.spmm_fn(csr, src[:, :W], dst[:, :W], (0, R), acc, "all", self._th)
             if exchanged:
                 works, src = new_works, full
             else:
