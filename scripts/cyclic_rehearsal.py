@@ -137,6 +137,8 @@ def main():
     ap.add_argument("--bw", default="300,450,600", help="assumed all-gather ingress GB/s per rank")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--ranks", default="all", help="'all' or a comma list of ranks to time")
+    ap.add_argument("--pad-input", default="auto", choices=["auto", "yes", "no"],
+                    help="re-lay X_0 into 128-B rows before hop 1 (auto: P <= 4)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="sgc_set_tuning knob (applies to every launch, single-GPU step included)")
     args = ap.parse_args()
@@ -164,7 +166,8 @@ def main():
                 recs = []
                 for r in ranks:
                     cp = LocalCyclic(S.row_ptr, S.col_idx, S.val, r, P, "cuda", tile=tile,
-                                     groups=G)
+                                     groups=G, pad_input={"auto": None, "yes": True,
+                                                          "no": False}[args.pad_input])
                     sh = cp.shard
                     t = timeit(lambda: cp.propagate(X0, K, output="sharded"), args.reps)
                     torch.cuda.synchronize()
@@ -176,8 +179,9 @@ def main():
                     plan = launch_plan(K, G)
                     ci = sh.csr_input
                     th, hb = cp._th  # the rank-level thresholds every launch used
+                    pad = P <= 4 if args.pad_input == "auto" else args.pad_input == "yes"
                     has_hub = [ci.plan(c * sh.group_rows, (c + 1) * sh.group_rows, th, hb,
-                                       Fp if P <= 4 else F).n_hub > 0  # hop-1 width
+                                       Fp if pad else F).n_hub > 0  # hop-1 width
                                for c in range(G)]
                     dur = durations(plan, light, hub, has_hub)
                     gbytes = P * sh.group_rows * Fp * 4

@@ -512,7 +512,6 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
 // nonzeros of the loader's run) halves the bytes each block ingests per
 // nonzero and spreads a hub over twice the CUs; it needs 128-B aligned X rows
 // to stay one line per segment.
-constexpr int kHubLoaders = 15;
 constexpr int kHubInstr = 16;  // consecutive nonzeros per loader lane per round
 constexpr int kHubDepth = 3;   // rounds held in loader registers (17 loads each: vmcnt <= 63)
 constexpr int kHubUnroll = 6;  // lcm(kHubDepth, 2): X ring slot and colv parity compile-time
@@ -527,11 +526,11 @@ constexpr int kHubPre = SGC_HUB_PRE;  // LDS batches of 4 nonzeros the chain rea
 #define SGC_HUB_SCHED 0
 #endif
 
-template <int HC>
+template <int HC, int NL>
 struct HubShape {
     static constexpr int kSegs = kWave / HC;                     // nonzero runs per loader wave
     static constexpr int kPerLoader = kHubInstr * kSegs;         // nonzeros per loader per round
-    static constexpr int kRound = kHubLoaders * kPerLoader;      // nonzeros per round (240 / 480)
+    static constexpr int kRound = NL * kPerLoader;               // nonzeros per round (240 / 480 at NL = 15)
     // chain read-ahead in batches of 4; HC = 64 fits at most 4 in 160 KB of LDS
     static constexpr int kPre = (HC == 64 && kHubPre > 4) ? 4 : kHubPre;
     static constexpr int kPad = 4 * kPre;                        // read-ahead past kRound
@@ -655,12 +654,15 @@ __device__ __forceinline__ void hub_chain_asm(float &acc, uint32_t xa, uint32_t 
 }
 #endif
 
-template <int HC>
-__global__ __launch_bounds__(1024) void spmm_hub_kernel(
+// NL loader waves + the chain wave per workgroup: 15 (1024 threads, ~133 KB
+// of LDS: one workgroup per CU) or 7 (512 threads, ~68 KB: two per CU, half
+// the CU held per hub chain; sgc_set_tuning("hub_loaders")).
+template <int HC, int NL>
+__global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy, int row_begin,
     int F, const int *__restrict__ hub_rows, int n_chunks, int accum) {
-    using Sh = HubShape<HC>;
+    using Sh = HubShape<HC, NL>;
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) float gxT[2][HC * Sh::kStride];  // 2 x 66.5 KB
     __shared__ __attribute__((aligned(16))) float gv[2][Sh::kRound + Sh::kPad];  // + read-ahead
@@ -1066,6 +1068,9 @@ static int g_hub_first = 0;
 // shorter than that synchronisation: Pubmed shape 70 -> 61 us per hop).
 // Set through sgc_set_tuning("hub_stream").
 static int g_hub_stream = 0;
+// Loader waves per hub workgroup: 15 or 7 (spmm_hub_kernel).  Set through
+// sgc_set_tuning("hub_loaders").
+static int g_hub_loaders = 15;
 
 int set_tuning(const char *key, int64_t value) {
     SGC_REQUIRE(key, SGC_EINVAL, "set_tuning: null key");
@@ -1088,6 +1093,11 @@ int set_tuning(const char *key, int64_t value) {
     if (std::string(key) == "hub_first") {
         SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "hub_first must be 0 or 1");
         g_hub_first = (int)value;
+        return SGC_OK;
+    }
+    if (std::string(key) == "hub_loaders") {
+        SGC_REQUIRE(value == 7 || value == 15, SGC_EINVAL, "hub_loaders must be 7 or 15");
+        g_hub_loaders = (int)value;
         return SGC_OK;
     }
     if (std::string(key) == "hub_stream") {
@@ -1124,6 +1134,7 @@ int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "hub_priority") return g_hub_priority;
     if (key && std::string(key) == "hub_first") return g_hub_first;
     if (key && std::string(key) == "hub_stream") return g_hub_stream;
+    if (key && std::string(key) == "hub_loaders") return g_hub_loaders;
     return -1;
 }
 
@@ -1187,14 +1198,19 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             SGC_HIP_CHECK(pooled_event(&tl.h1));
             SGC_HIP_CHECK(hipEventRecord(tl.h0, hs));
         }
-        if (hc == 32)
-            hipLaunchKernelGGL(spmm_hub_kernel<32>, dim3((unsigned)(n_hub * n_chunks)), dim3(1024),
-                               0, hs, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
-                               (int)F, heavy_rows, n_chunks, accum);
-        else
-            hipLaunchKernelGGL(spmm_hub_kernel<64>, dim3((unsigned)(n_hub * n_chunks)), dim3(1024),
-                               0, hs, row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin,
-                               (int)F, heavy_rows, n_chunks, accum);
+        const dim3 hub_grid((unsigned)(n_hub * n_chunks));
+#define SGC_LAUNCH_HUB(HCV, NLV)                                                             \
+    hipLaunchKernelGGL((spmm_hub_kernel<HCV, NLV>), hub_grid, dim3(64 * (NLV + 1)), 0, hs,   \
+                       row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)F,        \
+                       heavy_rows, n_chunks, accum)
+        if (hc == 32) {
+            if (g_hub_loaders == 7) SGC_LAUNCH_HUB(32, 7);
+            else SGC_LAUNCH_HUB(32, 15);
+        } else {
+            if (g_hub_loaders == 7) SGC_LAUNCH_HUB(64, 7);
+            else SGC_LAUNCH_HUB(64, 15);
+        }
+#undef SGC_LAUNCH_HUB
         SGC_HIP_CHECK(hipGetLastError());
         if (timing) SGC_HIP_CHECK(hipEventRecord(tl.h1, hs));
         heavy_rows += n_hub;

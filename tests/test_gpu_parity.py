@@ -256,7 +256,8 @@ def test_rmat_shape_hash(shapes_golden, shape_rows):
 
 @pytest.mark.parametrize("F", [64, 130, 192])
 @pytest.mark.parametrize("hub_chunk", [32, 64])
-def test_long_hub_rows_bit_exact(oracle, F, hub_chunk):
+@pytest.mark.parametrize("hub_loaders", [15, 7])
+def test_long_hub_rows_bit_exact(oracle, F, hub_chunk, hub_loaders):
     """Hub rows of 7,000 / 3,001 / 2,881 nonzeros on the LDS-staged hub kernel:
     several kHubUnroll iterations (2,880 nonzeros each at HC=32), the
     register-ring and column-id parity wrap, and ragged last rounds, on
@@ -278,6 +279,7 @@ def test_long_hub_rows_bit_exact(oracle, F, hub_chunk):
     want = oracle.propagate(S.row_ptr, S.col_idx, S.val, X, 2)
     lib = _lib.load()
     _lib.check(lib.sgc_set_tuning(b"hub_chunk", hub_chunk), "set_tuning")
+    _lib.check(lib.sgc_set_tuning(b"hub_loaders", hub_loaders), "set_tuning")
     try:
         csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val)
         pl = csr.plan(0, n, 64, 1000, F)
@@ -289,6 +291,7 @@ def test_long_hub_rows_bit_exact(oracle, F, hub_chunk):
         assert bits_equal(out.cpu().numpy(), want)
     finally:
         lib.sgc_set_tuning(b"hub_chunk", 0)
+        lib.sgc_set_tuning(b"hub_loaders", 15)
 
 
 @pytest.mark.parametrize("F", [32, 36, 44, 76, 96, 100, 124, 152])
