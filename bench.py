@@ -399,8 +399,9 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
             return (4 * (r1 - r0 + 1) + 8 * nz + 4 * w * min(X.shape[0], nz) +
                     4 * w * (r1 - r0) * (2 if acc else 1))
 
+        groups = args.cyclic_groups or (1 if world <= 2 else 2 if world <= 4 else 3)
         prop = CyclicRowPropagator(S.row_ptr, S.col_idx, S.val, rank, world, dev,
-                                   tile=args.cyclic_tile, groups=args.cyclic_groups,
+                                   tile=args.cyclic_tile, groups=groups,
                                    host_staging=staging,
                                    spmm_fn=bracket(_cyclic_spmm, launch_bytes))
         sh = prop.shard
@@ -490,8 +491,10 @@ def main():
                          "(tiles, --col-blocks), round-robin row tiles with column-ordered "
                          "exchange (cyclic), the feature columns, or auto = rows vs tiles vs "
                          "cyclic timed on the node")
-    ap.add_argument("--cyclic-groups", type=int, default=3,
-                    help="N>1 cyclic: column groups (= all-gathers) per hop")
+    ap.add_argument("--cyclic-groups", type=int, default=0,
+                    help="N>1 cyclic: column groups (= all-gathers) per hop; 0 = by rank count "
+                         "(1 up to 2 ranks, 2 up to 4, else 3: the best of the one-GPU rehearsal, "
+                         "DESIGN.md 6.2b)")
     ap.add_argument("--cyclic-tile", type=int, default=64,
                     help="N>1 cyclic: rows per round-robin tile")
     ap.add_argument("--col-blocks", type=int, default=2,
