@@ -592,10 +592,12 @@ def main():
             e_c, _, _ = timed(built[0], 3, 1, True, dev)
             trials[cand] = (e_c / 3, built, t_c)
         best = min(trials, key=lambda c: (trials[c][0], c))
+        chosen = best
         _, (step, parallelism, unit_desc), tm = trials[best]
         parallelism += " [auto-selected: " + ", ".join(
             f"{c} {trials[c][0] * 1e3:.2f} ms" for c in cands) + "]"
     else:
+        chosen = args.partition
         step, parallelism, unit_desc = build_dist_step(args, S, X0, dev, rank, world, K,
                                                        args.output, tm)
     elapsed, step_ms, _ = timed(step, args.steps, args.warmup, True, dev,
@@ -603,9 +605,12 @@ def main():
                                 on_stop=lambda: tm.update(on=False))
     launch_ms = [s.elapsed_time(e) for s, e in tm["pairs"]]
     alt = None
-    if args.alt_steps > 0 and "tiles" not in parallelism:
+    if args.alt_steps > 0 and chosen != "tiles":  # tiles: sharded output only
+        import copy
+        a = copy.copy(args)
+        a.partition = chosen
         alt_mode = "replicated" if args.output == "sharded" else "sharded"
-        alt_step, alt_par, _ = build_dist_step(args, S, X0, dev, rank, world, K, alt_mode,
+        alt_step, alt_par, _ = build_dist_step(a, S, X0, dev, rank, world, K, alt_mode,
                                                {"on": False})
         e_alt, _, _ = timed(alt_step, args.alt_steps, 1, True, dev)
         alt = {"output": alt_mode, "parallelism": alt_par, "steps": args.alt_steps,
