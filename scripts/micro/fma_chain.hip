@@ -791,6 +791,213 @@ __global__ void ring_B64V7(float *out, long long *cyc, int iters, float vc) {
     if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 
+
+// v values by scalar buffer loads (three 16-value SGPR banks, loaded two
+// chunks ahead, streaming through a 2 MB buffer: scalar-cache misses), x by
+// ds_read_b128 (the next 16 nonzeros' half while this half's FMAs run); one
+// lgkmcnt(0) per 16 nonzeros (scalar loads complete out of order).
+__global__ void ring_XS(float *out, long long *cyc, int iters, const float *vals) {
+    __shared__ __attribute__((aligned(16))) float x[64 * 260];
+    for (int i = threadIdx.x; i < 64 * 260; i += blockDim.x) x[i] = 1e-3f * (i % 97);
+    __syncthreads();
+    typedef __attribute__((address_space(3))) const float lds_f;
+    uint32_t xa = (uint32_t)(size_t)(lds_f *)(&x[threadIdx.x * 260]);
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    const uint64_t base = (uint64_t)vals;
+    i4 rs;
+    rs[0] = __builtin_amdgcn_readfirstlane((int)(base & 0xffffffffu));
+    rs[1] = __builtin_amdgcn_readfirstlane((int)(base >> 32));
+    rs[2] = 0x200000;  // num_records (bytes)
+    rs[3] = 0x00020000;
+    uint32_t vo = 0;
+    float acc = 0;
+    int it = iters;
+    long long t0 = __builtin_amdgcn_s_memtime();
+    asm volatile(
+            "s_waitcnt lgkmcnt(0)\n"
+            "s_buffer_load_dwordx16 s[40:55], %[rs], %[vo]\n"
+            "s_add_u32 %[vo], %[vo], 64\n"
+            "s_buffer_load_dwordx16 s[56:71], %[rs], %[vo]\n"
+            "s_add_u32 %[vo], %[vo], 64\n"
+            "ds_read_b128 v[80:83], %[xa] offset:0\n"
+            "ds_read_b128 v[84:87], %[xa] offset:16\n"
+            "ds_read_b128 v[88:91], %[xa] offset:32\n"
+            "ds_read_b128 v[92:95], %[xa] offset:48\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "1:\n"
+            "ds_read_b128 v[96:99], %[xa] offset:64\n"
+            "ds_read_b128 v[100:103], %[xa] offset:80\n"
+            "ds_read_b128 v[104:107], %[xa] offset:96\n"
+            "ds_read_b128 v[108:111], %[xa] offset:112\n"
+            "s_buffer_load_dwordx16 s[72:87], %[rs], %[vo]\n"
+            "s_add_u32 %[vo], %[vo], 64\n"
+            "s_and_b32 %[vo], %[vo], 0x1fffff\n"
+            "v_fmac_f32 %[acc], s40, v80\n"
+            "v_fmac_f32 %[acc], s41, v81\n"
+            "v_fmac_f32 %[acc], s42, v82\n"
+            "v_fmac_f32 %[acc], s43, v83\n"
+            "v_fmac_f32 %[acc], s44, v84\n"
+            "v_fmac_f32 %[acc], s45, v85\n"
+            "v_fmac_f32 %[acc], s46, v86\n"
+            "v_fmac_f32 %[acc], s47, v87\n"
+            "v_fmac_f32 %[acc], s48, v88\n"
+            "v_fmac_f32 %[acc], s49, v89\n"
+            "v_fmac_f32 %[acc], s50, v90\n"
+            "v_fmac_f32 %[acc], s51, v91\n"
+            "v_fmac_f32 %[acc], s52, v92\n"
+            "v_fmac_f32 %[acc], s53, v93\n"
+            "v_fmac_f32 %[acc], s54, v94\n"
+            "v_fmac_f32 %[acc], s55, v95\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "ds_read_b128 v[80:83], %[xa] offset:64\n"
+            "ds_read_b128 v[84:87], %[xa] offset:80\n"
+            "ds_read_b128 v[88:91], %[xa] offset:96\n"
+            "ds_read_b128 v[92:95], %[xa] offset:112\n"
+            "s_buffer_load_dwordx16 s[40:55], %[rs], %[vo]\n"
+            "s_add_u32 %[vo], %[vo], 64\n"
+            "s_and_b32 %[vo], %[vo], 0x1fffff\n"
+            "v_fmac_f32 %[acc], s56, v96\n"
+            "v_fmac_f32 %[acc], s57, v97\n"
+            "v_fmac_f32 %[acc], s58, v98\n"
+            "v_fmac_f32 %[acc], s59, v99\n"
+            "v_fmac_f32 %[acc], s60, v100\n"
+            "v_fmac_f32 %[acc], s61, v101\n"
+            "v_fmac_f32 %[acc], s62, v102\n"
+            "v_fmac_f32 %[acc], s63, v103\n"
+            "v_fmac_f32 %[acc], s64, v104\n"
+            "v_fmac_f32 %[acc], s65, v105\n"
+            "v_fmac_f32 %[acc], s66, v106\n"
+            "v_fmac_f32 %[acc], s67, v107\n"
+            "v_fmac_f32 %[acc], s68, v108\n"
+            "v_fmac_f32 %[acc], s69, v109\n"
+            "v_fmac_f32 %[acc], s70, v110\n"
+            "v_fmac_f32 %[acc], s71, v111\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "ds_read_b128 v[96:99], %[xa] offset:64\n"
+            "ds_read_b128 v[100:103], %[xa] offset:80\n"
+            "ds_read_b128 v[104:107], %[xa] offset:96\n"
+            "ds_read_b128 v[108:111], %[xa] offset:112\n"
+            "s_buffer_load_dwordx16 s[56:71], %[rs], %[vo]\n"
+            "s_add_u32 %[vo], %[vo], 64\n"
+            "s_and_b32 %[vo], %[vo], 0x1fffff\n"
+            "v_fmac_f32 %[acc], s72, v80\n"
+            "v_fmac_f32 %[acc], s73, v81\n"
+            "v_fmac_f32 %[acc], s74, v82\n"
+            "v_fmac_f32 %[acc], s75, v83\n"
+            "v_fmac_f32 %[acc], s76, v84\n"
+            "v_fmac_f32 %[acc], s77, v85\n"
+            "v_fmac_f32 %[acc], s78, v86\n"
+            "v_fmac_f32 %[acc], s79, v87\n"
+            "v_fmac_f32 %[acc], s80, v88\n"
+            "v_fmac_f32 %[acc], s81, v89\n"
+            "v_fmac_f32 %[acc], s82, v90\n"
+            "v_fmac_f32 %[acc], s83, v91\n"
+            "v_fmac_f32 %[acc], s84, v92\n"
+            "v_fmac_f32 %[acc], s85, v93\n"
+            "v_fmac_f32 %[acc], s86, v94\n"
+            "v_fmac_f32 %[acc], s87, v95\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "ds_read_b128 v[80:83], %[xa] offset:64\n"
+            "ds_read_b128 v[84:87], %[xa] offset:80\n"
+            "ds_read_b128 v[88:91], %[xa] offset:96\n"
+            "ds_read_b128 v[92:95], %[xa] offset:112\n"
+            "s_buffer_load_dwordx16 s[72:87], %[rs], %[vo]\n"
+            "s_add_u32 %[vo], %[vo], 64\n"
+            "s_and_b32 %[vo], %[vo], 0x1fffff\n"
+            "v_fmac_f32 %[acc], s40, v96\n"
+            "v_fmac_f32 %[acc], s41, v97\n"
+            "v_fmac_f32 %[acc], s42, v98\n"
+            "v_fmac_f32 %[acc], s43, v99\n"
+            "v_fmac_f32 %[acc], s44, v100\n"
+            "v_fmac_f32 %[acc], s45, v101\n"
+            "v_fmac_f32 %[acc], s46, v102\n"
+            "v_fmac_f32 %[acc], s47, v103\n"
+            "v_fmac_f32 %[acc], s48, v104\n"
+            "v_fmac_f32 %[acc], s49, v105\n"
+            "v_fmac_f32 %[acc], s50, v106\n"
+            "v_fmac_f32 %[acc], s51, v107\n"
+            "v_fmac_f32 %[acc], s52, v108\n"
+            "v_fmac_f32 %[acc], s53, v109\n"
+            "v_fmac_f32 %[acc], s54, v110\n"
+            "v_fmac_f32 %[acc], s55, v111\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "ds_read_b128 v[96:99], %[xa] offset:64\n"
+            "ds_read_b128 v[100:103], %[xa] offset:80\n"
+            "ds_read_b128 v[104:107], %[xa] offset:96\n"
+            "ds_read_b128 v[108:111], %[xa] offset:112\n"
+            "s_buffer_load_dwordx16 s[40:55], %[rs], %[vo]\n"
+            "s_add_u32 %[vo], %[vo], 64\n"
+            "s_and_b32 %[vo], %[vo], 0x1fffff\n"
+            "v_fmac_f32 %[acc], s56, v80\n"
+            "v_fmac_f32 %[acc], s57, v81\n"
+            "v_fmac_f32 %[acc], s58, v82\n"
+            "v_fmac_f32 %[acc], s59, v83\n"
+            "v_fmac_f32 %[acc], s60, v84\n"
+            "v_fmac_f32 %[acc], s61, v85\n"
+            "v_fmac_f32 %[acc], s62, v86\n"
+            "v_fmac_f32 %[acc], s63, v87\n"
+            "v_fmac_f32 %[acc], s64, v88\n"
+            "v_fmac_f32 %[acc], s65, v89\n"
+            "v_fmac_f32 %[acc], s66, v90\n"
+            "v_fmac_f32 %[acc], s67, v91\n"
+            "v_fmac_f32 %[acc], s68, v92\n"
+            "v_fmac_f32 %[acc], s69, v93\n"
+            "v_fmac_f32 %[acc], s70, v94\n"
+            "v_fmac_f32 %[acc], s71, v95\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "ds_read_b128 v[80:83], %[xa] offset:64\n"
+            "ds_read_b128 v[84:87], %[xa] offset:80\n"
+            "ds_read_b128 v[88:91], %[xa] offset:96\n"
+            "ds_read_b128 v[92:95], %[xa] offset:112\n"
+            "s_buffer_load_dwordx16 s[56:71], %[rs], %[vo]\n"
+            "s_add_u32 %[vo], %[vo], 64\n"
+            "s_and_b32 %[vo], %[vo], 0x1fffff\n"
+            "v_fmac_f32 %[acc], s72, v96\n"
+            "v_fmac_f32 %[acc], s73, v97\n"
+            "v_fmac_f32 %[acc], s74, v98\n"
+            "v_fmac_f32 %[acc], s75, v99\n"
+            "v_fmac_f32 %[acc], s76, v100\n"
+            "v_fmac_f32 %[acc], s77, v101\n"
+            "v_fmac_f32 %[acc], s78, v102\n"
+            "v_fmac_f32 %[acc], s79, v103\n"
+            "v_fmac_f32 %[acc], s80, v104\n"
+            "v_fmac_f32 %[acc], s81, v105\n"
+            "v_fmac_f32 %[acc], s82, v106\n"
+            "v_fmac_f32 %[acc], s83, v107\n"
+            "v_fmac_f32 %[acc], s84, v108\n"
+            "v_fmac_f32 %[acc], s85, v109\n"
+            "v_fmac_f32 %[acc], s86, v110\n"
+            "v_fmac_f32 %[acc], s87, v111\n"
+            "s_waitcnt lgkmcnt(0)\n"
+            "s_sub_u32 %[it], %[it], 1\n"
+            "s_cmp_lg_u32 %[it], 0\n"
+            "s_cbranch_scc1 1b\n"
+            "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [it] "+s"(it), [vo] "+s"(vo)
+        : [xa] "v"(xa), [rs] "s"(rs)
+        : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "scc");
+    long long t1 = __builtin_amdgcn_s_memtime();
+    out[threadIdx.x] = acc;
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
+int main5() {
+    float *out, *vals;
+    long long *cyc, h;
+    (void)hipMalloc(&out, 1024 * 4);
+    (void)hipMalloc(&cyc, 8);
+    (void)hipMalloc(&vals, 0x200000);
+    (void)hipMemset(vals, 0, 0x200000);
+    const int iters = 20000;  // x 6 x 16 nonzeros
+    for (int k = 0; k < 2; ++k)
+        hipLaunchKernelGGL(ring_XS, dim3(1), dim3(64), 0, 0, out, cyc, iters, (const float *)vals);
+    (void)hipMemcpy(&h, cyc, 8, hipMemcpyDeviceToHost);
+    printf("{\"case\": \"%s\", \"cycles_per_nonzero\": %.2f}\n",
+           "x b128 half-ring + v by s_buffer_load_dwordx16 (3 banks, 2 ahead)",
+           (double)h / (iters * 96.0));
+    return 0;
+}
+
 int main4() {
     float *out;
     long long *cyc, h;
@@ -806,7 +1013,7 @@ int main4() {
     RUN4(ring_B64x14, 28, "asm ring 14 x ds_read_b64, v in SGPR")
     RUN4(ring_B32x14, 14, "asm ring 14 x ds_read_b32, v in SGPR")
     RUN4(ring_B64V7, 14, "asm ring 7 x (x ds_read_b64 + v ds_read_b64)")
-    return 0;
+    return main5();
 }
 
 int main3() {
