@@ -17,9 +17,11 @@ work fixed, so scaling is "strong":
   --partition cyclic  row tiles dealt round-robin; each all-gather carries one
                 column group (--cyclic-groups G) and the next hop consumes it
                 as it arrives (column-group passes, SGC_SPMM_ACCUMULATE)
-  --partition auto (default)  rows vs tiles vs cyclic, timed on the node
   --partition features  each rank runs all K hops on its block of feature
-                columns over the full S, no exchange between hops
+                columns over the full S, no exchange between hops; sharded
+                output by one all-to-all of the row blocks of X_K
+  --partition auto (default)  rows vs cyclic vs features (vs tiles), timed
+                on the node (max over ranks); the fastest is kept
   --output sharded (default)  each rank ends with its row block of X_K
   --output replicated  every rank ends with all of X_K (one more all-gather)
 The other output mode is timed too (`alt_output`, --alt-steps).
@@ -489,8 +491,8 @@ def main():
                     choices=["auto", "rows", "tiles", "cyclic", "features"],
                     help="N>1: split the rows of S (per-hop all-gather), rows x feature blocks "
                          "(tiles, --col-blocks), round-robin row tiles with column-ordered "
-                         "exchange (cyclic), the feature columns, or auto = rows vs tiles vs "
-                         "cyclic timed on the node")
+                         "exchange (cyclic), the feature columns (no exchange between hops, "
+                         "one all-to-all at the end), or auto = all of them timed on the node")
     ap.add_argument("--cyclic-groups", type=int, default=0,
                     help="N>1 cyclic: column groups (= all-gathers) per hop; 0 = by rank count "
                          "(1 up to 2 ranks, 2 up to 4, else 3: the best of the one-GPU rehearsal, "
@@ -580,7 +582,7 @@ def main():
         # row partition vs 2-D tiles: timed on this node (max over ranks), so
         # the exchange rate the node actually has decides, not an estimate
         import copy
-        cands = ["rows", "cyclic"]
+        cands = ["rows", "cyclic", "features"]
         if world >= 4 and world % args.col_blocks == 0 and args.output == "sharded":
             cands.append("tiles")
         trials = {}

@@ -62,7 +62,12 @@ const char *sgc_last_error(void);
  *   "rows_per_wave": light rows per wavefront when 16-B lanes are possible
  *                   (0 = default, auto; 2 = 32 lanes x 4 floats per row; 4 =
  *                   16 lanes; 1 = one row per wave with the slice_floats /
- *                   max_vec scheme).
+ *                   max_vec scheme);
+ *   "heavy_packed": 1 = heavy rows of the multi-row light kernel packed
+ *                   64/LR per wavefront like light rows; 0 = one wavefront
+ *                   per 64*VH-float sub-chunk of a heavy row (default);
+ *   "hub_loaders":  loader waves per hub workgroup, 15 (default) or 7;
+ *   "light_lds":    dynamic LDS bytes reserved per light workgroup (0).
  * sgc_get_tuning returns -1 for an unknown key. */
 int sgc_set_tuning(const char *key, int64_t value);
 int64_t sgc_get_tuning(const char *key);

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--hub-chunk", default="0")
     ap.add_argument("--hub-priority", default="0")
     ap.add_argument("--slices", default="128", help="slice_floats values")
+    ap.add_argument("--heavy-packed", default="0", help="heavy_packed values")
     ap.add_argument("--hubs", default="auto", help="hub thresholds per case ('auto' = default)")
     ap.add_argument("--heavies", default="default", help="heavy-row thresholds per case")
     ap.add_argument("--shape", default="reddit")
@@ -71,12 +72,15 @@ def main():
     hcs = [int(x) for x in args.hub_chunk.split(",")]
     hps = [int(x) for x in args.hub_priority.split(",")]
     sfs = [int(x) for x in args.slices.split(",")]
-    variants = [(f"{name}/hc{hc}/hp{hp}/s{sf}", lib, (mv, hc, hp, sf)) for name, lib in loaded
-                for mv in mvs for hc in hcs for hp in hps for sf in sfs]
+    hks = [int(x) for x in args.heavy_packed.split(",")]
+    variants = [(f"{name}/hc{hc}/hp{hp}/s{sf}/pk{pk}", lib, (mv, hc, hp, sf, pk))
+                for name, lib in loaded
+                for mv in mvs for hc in hcs for hp in hps for sf in sfs for pk in hks]
 
     def run(lib, cfg, c):
-        mv, hc, hp, sf = cfg
+        mv, hc, hp, sf, pk = cfg
         lib.sgc_set_tuning(b"slice_floats", sf)
+        lib.sgc_set_tuning(b"heavy_packed", pk)
         _, Xw, ld, w, r0, r1, pl, Y, _ = c
         lib.sgc_set_tuning(b"max_vec", mv)
         lib.sgc_set_tuning(b"hub_chunk", hc)

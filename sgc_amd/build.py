@@ -29,7 +29,6 @@ FLAGS = [
     "-O3",
     "-std=c++17",
     "-fPIC",
-    "-shared",
     # IEEE fp32: no FTZ, no contraction beyond the explicit fmaf chains
     "-fno-gpu-flush-denormals-to-zero",
     "-ffp-contract=off",
@@ -52,14 +51,26 @@ def build(force=False, verbose=True, out=None, defines=()):
     lib = out or LIB
     if not force and out is None and not _stale():
         return LIB
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     tmp = lib + ".tmp"
     os.makedirs(os.path.dirname(lib), exist_ok=True)
-    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-I", os.path.join(ROOT, "include"),
-           "-I", CSRC, *srcs, "-o", tmp]
-    if verbose:
-        print("[sgc_amd] " + " ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
+    common = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-I", os.path.join(ROOT, "include"),
+              "-I", CSRC]
+    # one hipcc per source, in parallel (each source launches only its own
+    # kernels, so no relocatable device code is needed), then one link
+    with tempfile.TemporaryDirectory(prefix="sgc_amd_build_") as td:
+        objs = [os.path.join(td, os.path.basename(s) + ".o") for s in srcs]
+        cmds = [[*common, "-c", s, "-o", o] for s, o in zip(srcs, objs)]
+        if verbose:
+            print("[sgc_amd] " + " ".join(cmds[0][:-4]) + " -c <source> (x%d, parallel)"
+                  % len(cmds), file=sys.stderr)
+        jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+        with ThreadPoolExecutor(jobs) as ex:
+            for f in [ex.submit(subprocess.check_call, c) for c in cmds]:
+                f.result()
+        subprocess.check_call([HIPCC, *FLAGS, "-shared", *objs, "-o", tmp])
     os.replace(tmp, lib)
     return lib
 

@@ -340,8 +340,15 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 //    longest; lanes past their row's end re-load their row's last nonzero
 //    (same lines, never out of bounds) and skip the FMAs -- still one
 //    sequential FMA chain per element in CSR order.
-// Heavy items (rows above heavy_threshold, one wave per 64*VH-float
-// sub-chunk, n_sub per slice) come first in the grid, as in spmm_csr_kernel.
+// Heavy items (rows above heavy_threshold) come first in the grid, as in
+// spmm_csr_kernel, in one of two forms:
+//  * packed (heavy_packed = 1): R heavy rows per wave, exactly like
+//    light rows (LR lanes and 16-B loads each), taken R at a time from the
+//    plan's list, which is sorted by length, so the rows sharing a wave have
+//    about the same length;
+//  * one wave per 64*VH-float sub-chunk, n_sub per slice (heavy_packed = 0,
+//    the default): 8-B lanes at F % 4 != 0, one row per load instruction,
+//    but twice the loads in flight per row.
 constexpr int kRowsU = 4;
 
 template <int LB, int VH, int UH>
@@ -349,7 +356,8 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
     int row_begin, int n_rows, int F, int F_load, int LR, int vec_store, int n_sub,
-    const int *__restrict__ heavy_rows, int n_heavy, int heavy_threshold, int accum) {
+    const int *__restrict__ heavy_rows, int n_heavy, int heavy_threshold, int accum,
+    int heavy_packed) {
     constexpr int V = 4, U = kRowsU;
     constexpr int kSteps = LB / U;  // steps per LDS block
     static_assert(kSteps >= 2 && kSteps % 2 == 0, "bad block");
@@ -361,8 +369,9 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const int wl = threadIdx.x / kWave;
     const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kBlock / kWave) + wl));
     const int slice = blockIdx.y;
-    const int n_heavy_items = n_heavy * n_sub;
-    if (wave < n_heavy_items) {
+    const int R = kWave / LR;  // rows per wave (uniform)
+    const int n_heavy_items = heavy_packed ? (n_heavy + R - 1) / R : n_heavy * n_sub;
+    if (!heavy_packed && wave < n_heavy_items) {
         const int h = wave / n_sub;
         const int sub = slice * n_sub + (wave - h * n_sub);  // in units of 64*VH floats
         if (sub * kWave * VH >= F) return;
@@ -373,18 +382,28 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
                                         accum != 0);
         return;
     }
-    const int R = kWave / LR;  // rows per wave (uniform)
-    const int w = wave - n_heavy_items;
-    if (w * R >= n_rows) return;  // wave-uniform
     const int sub = lane / LR, l = lane - sub * LR;
-    const int r = w * R + sub;
-    int k0 = 0, len = 0;
+    int r = 0, k0 = 0, len = 0;
     bool mine = false;
-    if (sub < R && r < n_rows) {
-        k0 = row_ptr[row_begin + r];
-        const int d = row_ptr[row_begin + r + 1] - k0;
-        mine = d <= heavy_threshold;  // longer rows: heavy items / hub kernel
-        len = mine ? d : 0;
+    if (wave < n_heavy_items) {  // packed heavy rows: plan entries wave*R + sub
+        const int hi = wave * R + sub;
+        if (sub < R && hi < n_heavy) {
+            const int row = heavy_rows[hi];
+            r = row - row_begin;
+            k0 = row_ptr[row];
+            len = row_ptr[row + 1] - k0;
+            mine = true;
+        }
+    } else {
+        const int w = wave - n_heavy_items;
+        if (w * R >= n_rows) return;  // wave-uniform
+        r = w * R + sub;
+        if (sub < R && r < n_rows) {
+            k0 = row_ptr[row_begin + r];
+            const int d = row_ptr[row_begin + r + 1] - k0;
+            mine = d <= heavy_threshold;  // longer rows: heavy items / hub kernel
+            len = mine ? d : 0;
+        }
     }
     int n_max = 0;
     for (int s = 0; s < R; ++s) n_max = max(n_max, __builtin_amdgcn_readlane(len, s * LR));
@@ -1012,21 +1031,30 @@ static int g_max_vec = 4;
 // spmm_rows_kernel with 32 / 16 lanes per row on wide launches; 1 = never.
 // profiles/r02/sweep_rows*.  Set through sgc_set_tuning("rows_per_wave").
 static int g_rows_per_wave = 0;
+// Heavy rows in spmm_rows_kernel: 1 = packed R per wave like light rows, 0 =
+// one wave per 64*VH-float sub-chunk (default).  Packed measured equal at
+// F = 602 and 1.7x slower on a single 76-float slice, where the longest heavy
+// rows' latency is the hop's critical path and packing halves each row's
+// loads in flight (profiles/r02/packed_sweep.log).  Set through
+// sgc_set_tuning("heavy_packed").
+static int g_heavy_packed = 0;
 
 template <int LB, int VH>
 hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int R = kWave / LR, SW = LR * 4;
     const int slices = (F_load + SW - 1) / SW;
-    // heavy sub-chunks per slice: whole 64*VH-float chunks of a slice, or of
-    // the launch's width when it is a single slice
+    // heavy sub-chunks per slice (unpacked heavy rows): whole 64*VH-float
+    // chunks of a slice, or of the launch's width when it is a single slice
     const int n_sub = slices > 1 ? SW / (kWave * VH) : (F_load + kWave * VH - 1) / (kWave * VH);
-    const int64_t waves = (int64_t)a.n_heavy * n_sub + (a.n_rows + R - 1) / R;
+    const int64_t heavy_waves = g_heavy_packed ? ((int64_t)a.n_heavy + R - 1) / R
+                                               : (int64_t)a.n_heavy * n_sub;
+    const int64_t waves = heavy_waves + (a.n_rows + R - 1) / R;
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     dim3 grid((unsigned)blocks, (unsigned)slices);
     hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, SGC_HEAVY_U>), grid, dim3(kBlock), g_light_lds,
                        a.stream, a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
                        a.n_rows, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
-                       a.heavy_threshold, a.accum);
+                       a.heavy_threshold, a.accum, g_heavy_packed);
     return hipGetLastError();
 }
 
@@ -1111,6 +1139,11 @@ int set_tuning(const char *key, int64_t value) {
         g_rows_per_wave = (int)value;
         return SGC_OK;
     }
+    if (std::string(key) == "heavy_packed") {
+        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "heavy_packed must be 0 or 1");
+        g_heavy_packed = (int)value;
+        return SGC_OK;
+    }
     if (std::string(key) == "light_lds") {
         SGC_REQUIRE(value >= 0 && value <= 150 * 1024, SGC_EINVAL, "light_lds out of range");
         g_light_lds = (int)value;
@@ -1130,6 +1163,7 @@ int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "max_vec") return g_max_vec;
     if (key && std::string(key) == "rows_per_wave") return g_rows_per_wave;
     if (key && std::string(key) == "light_lds") return g_light_lds;
+    if (key && std::string(key) == "heavy_packed") return g_heavy_packed;
     if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
     if (key && std::string(key) == "hub_priority") return g_hub_priority;
     if (key && std::string(key) == "hub_first") return g_hub_first;

@@ -1136,13 +1136,14 @@ class FeaturePartitionedPropagator:
         else:
             src = X0[:, c0:c1]  # K = 1: read the block in place
         if output == "sharded":
-            # last hop per destination row block -> one all-to-all
+            # last hop -> one all-to-all.  Destination block q is rows
+            # [q*Bn, (q+1)*Bn) (equal_row_bounds), so ONE launch over all rows
+            # into send[:n] already lays the send buffer out by destination
+            # (a launch per block would pay the hub fork/join P times)
             Bn = max(1, -(-n // P))
             send = self._buf("send", (P * Bn, B), X0)
-            for q in range(P):
-                r0, r1 = int(rb[q]), int(rb[q + 1])
-                if w and r1 > r0:
-                    self.spmm_fn(src, r0, r1, send[q * Bn:q * Bn + (r1 - r0), :w])
+            if w and n:
+                self.spmm_fn(src, 0, n, send[:n, :w])
             recv = self._buf("recv", (P * Bn, B), X0)
             work = self._all_to_all(recv, send)
             if work is not None:
