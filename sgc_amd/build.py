@@ -51,7 +51,7 @@ def build(force=False, verbose=True, out=None, defines=()):
     lib = out or LIB
     if not force and out is None and not _stale():
         return LIB
-    import tempfile
+    import hashlib
     from concurrent.futures import ThreadPoolExecutor
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     tmp = lib + ".tmp"
@@ -60,17 +60,23 @@ def build(force=False, verbose=True, out=None, defines=()):
               "-I", CSRC]
     # one hipcc per source, in parallel (each source launches only its own
     # kernels, so no relocatable device code is needed), then one link
-    with tempfile.TemporaryDirectory(prefix="sgc_amd_build_") as td:
-        objs = [os.path.join(td, os.path.basename(s) + ".o") for s in srcs]
-        cmds = [[*common, "-c", s, "-o", o] for s, o in zip(srcs, objs)]
-        if verbose:
-            print("[sgc_amd] " + " ".join(cmds[0][:-4]) + " -c <source> (x%d, parallel)"
-                  % len(cmds), file=sys.stderr)
-        jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
-        with ThreadPoolExecutor(jobs) as ex:
-            for f in [ex.submit(subprocess.check_call, c) for c in cmds]:
-                f.result()
-        subprocess.check_call([HIPCC, *FLAGS, "-shared", *objs, "-o", tmp])
+    # objects in a fixed per-(output, defines) directory: the object paths
+    # end up in the code-object bundle, so a fixed path keeps the library
+    # byte-identical across rebuilds of the same sources (bench.py ties PMC
+    # traffic records to the library's sha256)
+    tag = hashlib.sha256(repr((os.path.abspath(lib), tuple(defines))).encode()).hexdigest()[:16]
+    td = os.path.join(ROOT, "build", f"obj_{tag}")  # git- and gpurun-ignored
+    os.makedirs(td, exist_ok=True)
+    objs = [os.path.join(td, os.path.basename(s) + ".o") for s in srcs]
+    cmds = [[*common, "-c", s, "-o", o] for s, o in zip(srcs, objs)]
+    if verbose:
+        print("[sgc_amd] " + " ".join(cmds[0][:-4]) + " -c <source> (x%d, parallel)"
+              % len(cmds), file=sys.stderr)
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with ThreadPoolExecutor(jobs) as ex:
+        for f in [ex.submit(subprocess.check_call, c) for c in cmds]:
+            f.result()
+    subprocess.check_call([HIPCC, *FLAGS, "-shared", *objs, "-o", tmp])
     os.replace(tmp, lib)
     return lib
 
