@@ -349,7 +349,11 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 //  * one wave per 64*VH-float sub-chunk, n_sub per slice (heavy_packed = 0,
 //    the default): 8-B lanes at F % 4 != 0, one row per load instruction,
 //    but twice the loads in flight per row.
-constexpr int kRowsU = 4;
+#ifndef SGC_ROWS_U
+#define SGC_ROWS_U 4  // nonzeros per row per step in spmm_rows_kernel (multiple of 4)
+#endif
+constexpr int kRowsU = SGC_ROWS_U;
+static_assert(kRowsU % 4 == 0, "rows kernel reads (col, val) four at a time");
 
 template <int LB, int VH, int UH>
 __global__ __launch_bounds__(256) void spmm_rows_kernel(
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     int row_begin, int n_rows, int F, int F_load, int LR, int vec_store, int n_sub,
     const int *__restrict__ heavy_rows, int n_heavy, int heavy_threshold, int accum,
     int heavy_packed) {
-    constexpr int V = 4, U = kRowsU;
+    constexpr int V = 4, U = kRowsU < LB / 2 ? kRowsU : LB / 2;
     constexpr int kSteps = LB / U;  // steps per LDS block
     static_assert(kSteps >= 2 && kSteps % 2 == 0, "bad block");
     typedef float f4 __attribute__((ext_vector_type(4)));
@@ -462,12 +466,18 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
         f4 xv[2][U];
         float vv[2][U];
         auto issue = [&](int buf, int i, int slot) {
-            const i4 cc = *reinterpret_cast<const i4 *>(&s_col[wl][buf][lds_row + i * U]);
-            const f4 vq = *reinterpret_cast<const f4 *>(&s_val[wl][buf][lds_row + i * U]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                vv[slot][u] = vq[u];
-                xv[slot][u] = *reinterpret_cast<const f4 *>(Xb + (int64_t)cc[u] * row_bytes + boff);
+            for (int q = 0; q < U / 4; ++q) {
+                const i4 cc =
+                    *reinterpret_cast<const i4 *>(&s_col[wl][buf][lds_row + i * U + 4 * q]);
+                const f4 vq =
+                    *reinterpret_cast<const f4 *>(&s_val[wl][buf][lds_row + i * U + 4 * q]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    vv[slot][4 * q + u] = vq[u];
+                    xv[slot][4 * q + u] =
+                        *reinterpret_cast<const f4 *>(Xb + (int64_t)cc[u] * row_bytes + boff);
+                }
             }
         };
         issue(0, 0, 0);
@@ -1269,7 +1279,15 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     const uintptr_t xa = reinterpret_cast<uintptr_t>(X), ya = reinterpret_cast<uintptr_t>(Y);
     const bool v4_ok = ldx % 4 == 0 && xa % 16 == 0 && F4 <= ldx && F4 >= 32 &&
                        (F4 == F || (flags & SGC_SPMM_X_PADDED));
-    const bool csr_v4 = F % 4 == 0 && pick_vec(F, ldx, ldy, X, Y) == 4;
+    // With both buffers padded, the one-row kernel may compute F rounded up
+    // to 4 as well: one 256-float slice (16-B lanes) covers a 129..256-float
+    // launch that the multi-row kernel would run as two passes (128 + the
+    // rest) -- e.g. a 146-column feature block at P = 4.  Wider launches keep
+    // the multi-row kernel's 128-float slices (Reddit's 602: MALL residency).
+    const bool pad_both = (flags & SGC_SPMM_X_PADDED) && (flags & SGC_SPMM_Y_PADDED);
+    const int64_t F_csr =
+        (F % 4 != 0 && pad_both && F4 > 128 && F4 <= 256 && F4 <= ldx && F4 <= ldy) ? F4 : F;
+    const bool csr_v4 = F_csr % 4 == 0 && pick_vec(F_csr, ldx, ldy, X, Y) == 4;
     // Small, wide launches (Cora shape: 2,708 rows x 1,433 features, X in
     // L2): latency-bound, so fewer and wider work items win -- the one-row
     // kernel with 512-float slices, 19.7 vs 24.9 us per hop for the
@@ -1305,8 +1323,9 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             e = vh2 ? launch_rows<8, 2>(a, (int)F4, LR, vec_store)
                     : launch_rows<8, 1>(a, (int)F4, LR, vec_store);
     } else {
-        const int V = pick_vec(F, ldx, ldy, X, Y);
-        const int chunks_total = (int)((F + kWave * V - 1) / (kWave * V));
+        const int V = pick_vec(F_csr, ldx, ldy, X, Y);
+        a.F = (int)(V == 4 ? F_csr : F);  // pad columns only with 16-B lanes
+        const int chunks_total = (int)((a.F + kWave * V - 1) / (kWave * V));
         const int cmax = max_chunks(V);
         const int sf = small_wide ? 512 : g_slice_floats;
         int C = sf > 0 ? std::max(1, sf / (kWave * V)) : cmax;

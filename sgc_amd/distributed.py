@@ -1066,13 +1066,14 @@ class FeaturePartitionedPropagator:
         self.group = group
         self.rank = dist.get_rank(group) if rank is None else int(rank)
         self.world_size = dist.get_world_size(group) if world_size is None else int(world_size)
+        self._padded_ok = spmm_fn is None  # the engine's own launches take pad flags
         if spmm_fn is None:
             if csr is None:
                 raise ValueError("FeaturePartitionedPropagator needs a DeviceCSR or an spmm_fn")
             from .propagate import spmm
 
-            def spmm_fn(X, r0, r1, out, _csr=csr):
-                return spmm(_csr, X, r0, r1, out=out)
+            def spmm_fn(X, r0, r1, out, flags=0, _csr=csr):
+                return spmm(_csr, X, r0, r1, out=out, flags=flags)
         self.csr = csr
         self.spmm_fn = spmm_fn
         self.chunks = max(1, int(chunks))
@@ -1123,18 +1124,33 @@ class FeaturePartitionedPropagator:
         if out is None:
             shape = (n, F) if output == "replicated" else (int(rb[p + 1] - rb[p]), F)
             out = torch.empty(shape, dtype=torch.float32, device=X0.device)
-        # hops 1..K-1 on the rank's column block, ping-pong in compact buffers
-        if K > 1:
+        from .propagate import SPMM_X_PADDED, SPMM_Y_PADDED
+
+        def hop(src, r0, r1, dst, own_src, own_dst):
+            # own buffers: 4-float pad columns may be read / written (16-B
+            # lanes at any block width); results never depend on it
+            if self._padded_ok:
+                fl = (SPMM_X_PADDED if own_src else 0) | (SPMM_Y_PADDED if own_dst else 0)
+                return self.spmm_fn(src, r0, r1, dst, flags=fl)
+            return self.spmm_fn(src, r0, r1, dst)
+
+        # hop 1 reads the caller's block in place when its rows are 16-B
+        # lanes already (w and c0 multiples of 4, 16-B aligned rows); else a
+        # compact 128-B-row copy first
+        inplace = (K == 1 or not X0.is_cuda or
+                   (w % 4 == 0 and c0 % 4 == 0 and X0.stride(0) % 4 == 0 and
+                    X0.data_ptr() % 16 == 0))
+        src, own = X0[:, c0:c1], False
+        if not inplace:
             a = self._buf("a", (n, ld), X0)
             _copy_cols(X0[:, c0:c1], a[:, :w])
-            src = a[:, :w]
-            for h in range(K - 1):
-                dst = self._buf(("h", h & 1), (n, ld), X0)[:, :w]
-                if w and n:
-                    self.spmm_fn(src, 0, n, dst)
-                src = dst
-        else:
-            src = X0[:, c0:c1]  # K = 1: read the block in place
+            src, own = a[:, :w], True
+        # hops 1..K-1 on the rank's column block, ping-pong in compact buffers
+        for h in range(K - 1):
+            dst = self._buf(("h", h & 1), (n, ld), X0)[:, :w]
+            if w and n:
+                hop(src, 0, n, dst, own, True)
+            src, own = dst, True
         if output == "sharded":
             # last hop -> one all-to-all.  Destination block q is rows
             # [q*Bn, (q+1)*Bn) (equal_row_bounds), so ONE launch over all rows
@@ -1142,8 +1158,8 @@ class FeaturePartitionedPropagator:
             # (a launch per block would pay the hub fork/join P times)
             Bn = max(1, -(-n // P))
             send = self._buf("send", (P * Bn, B), X0)
-            if w and n:
-                self.spmm_fn(src, 0, n, send[:n, :w])
+            if w and n:  # send's columns w..B-1 are never unpacked: pad-writable
+                hop(src, 0, n, send[:n, :w], own, True)
             recv = self._buf("recv", (P * Bn, B), X0)
             work = self._all_to_all(recv, send)
             if work is not None:
@@ -1160,7 +1176,7 @@ class FeaturePartitionedPropagator:
             rows = r1 - r0
             loc = self._buf(("loc", ci), (rows, B), X0)
             if w and rows:
-                self.spmm_fn(src, r0, r1, loc[:, :w])
+                hop(src, r0, r1, loc[:, :w], own, True)
             full = self._buf(("full", ci), (P * rows, B), X0)
             pending.append((r0, r1, full, self._all_gather(full, loc) if rows else None))
         for r0, r1, full, work in pending:

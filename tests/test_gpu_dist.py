@@ -162,3 +162,43 @@ def test_cyclic_partition_reddit_shape_hash(shapes_golden, groups):
     out = cp.propagate(torch.from_numpy(X).cuda(), 2, output="replicated")
     torch.cuda.synchronize()
     assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == g["outputs"]["2"]["sha"]
+
+
+@pytest.mark.parametrize("shape,P,K", [("pubmed", 8, 2), ("pubmed", 3, 3), ("cora", 8, 2)])
+def test_feature_partition_rank_steps_gpu(shape, P, K):
+    """Every rank's step of the feature partition on the HIP kernels (the
+    exchange replaced by capturing the all-to-all's send buffer): hop 1 in
+    place on the caller's block when it is 16-B laned (Pubmed's 64/52 and
+    168/164-column blocks, Cora's 180), through the compact copy otherwise
+    (Cora's last, 173 columns), pad-flagged hops in the engine's buffers, the one-launch
+    last hop laid out by destination -- equal to those columns and rows of the
+    single-GPU result (pinned to the reference's hashes elsewhere)."""
+    from sgc_amd import graphs
+    from sgc_amd.distributed import (FeaturePartitionedPropagator, equal_row_bounds,
+                                     feature_bounds)
+    from sgc_amd.propagate import DeviceCSR, propagate
+
+    class Capture(FeaturePartitionedPropagator):
+        def _all_to_all(self, recv, send):
+            self.sent = send.clone()
+            recv.copy_(send)
+            return None
+
+    S = graphs.synthetic_graph(shape, seed=0)
+    F = graphs.SHAPES[shape]["features"]
+    X = torch.from_numpy(graphs.synthetic_features(shape, S.n, F, seed=1)).cuda()
+    csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device="cuda")
+    full = propagate(csr, X, K)
+    fb, B = feature_bounds(F, P)
+    rb = equal_row_bounds(S.n, P)
+    Bn = -(-S.n // P)
+    for p in range(P):
+        c0, c1 = int(fb[p]), int(fb[p + 1])
+        prop = Capture(csr, rank=p, world_size=P)
+        for _ in range(2):  # buffers reused
+            prop.propagate(X, K, output="sharded")
+            torch.cuda.synchronize()
+            for q in range(P):
+                r0, r1 = int(rb[q]), int(rb[q + 1])
+                got = prop.sent[q * Bn:q * Bn + (r1 - r0), :c1 - c0]
+                assert torch.equal(got, full[r0:r1, c0:c1]), (p, q)
