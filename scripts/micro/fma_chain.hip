@@ -981,6 +981,117 @@ __global__ void ring_XS(float *out, long long *cyc, int iters, const float *vals
     if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 
+// S values off the LDS-read path by DPP: one ds_read_b32 per 16 nonzeros
+// (lane l holds v[l & 15], so every 16-lane row has all 16) and each FMA
+// broadcasts lane k of its row with row_newbcast:k; X as in ring_X8 (b128
+// ring, 8 batches = 2 iterations ahead).  Same FMA order and operands as the
+// hub chain: acc = fma(v[k], x[k], acc).
+__global__ void ring_XDPP(float *out, long long *cyc, int iters, float vc) {
+    __shared__ __attribute__((aligned(16))) float x[64 * 260];
+    __shared__ __attribute__((aligned(16))) float v[512];
+    for (int i = threadIdx.x; i < 64 * 260; i += blockDim.x) x[i] = 1e-3f * (i % 97);
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) v[i] = 0.5f + 1e-3f * i;
+    __syncthreads();
+    typedef __attribute__((address_space(3))) const float lds_f;
+    uint32_t xa = (uint32_t)(size_t)(lds_f *)(&x[threadIdx.x * 260]);
+    uint32_t vl = (uint32_t)(size_t)(lds_f *)(&v[threadIdx.x & 15]);
+    float acc = 0;
+    int it = iters;
+    (void)vc;
+    long long t0 = __builtin_amdgcn_s_memtime();
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n"
+        "ds_read_b32 v112, %[vl] offset:0\n"
+        "ds_read_b128 v[80:83], %[xa] offset:0\n"
+        "ds_read_b128 v[84:87], %[xa] offset:16\n"
+        "ds_read_b128 v[88:91], %[xa] offset:32\n"
+        "ds_read_b128 v[92:95], %[xa] offset:48\n"
+        "ds_read_b32 v113, %[vl] offset:64\n"
+        "ds_read_b128 v[96:99], %[xa] offset:64\n"
+        "ds_read_b128 v[100:103], %[xa] offset:80\n"
+        "ds_read_b128 v[104:107], %[xa] offset:96\n"
+        "ds_read_b128 v[108:111], %[xa] offset:112\n"
+        "1:\n"
+        // iteration A: v112, slots v80..v95
+        "s_waitcnt lgkmcnt(8)\n"
+        "v_fmac_f32_dpp %[acc], v112, v80 row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v81 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v82 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v83 row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[80:83], %[xa] offset:128\n"
+        "s_waitcnt lgkmcnt(8)\n"
+        "v_fmac_f32_dpp %[acc], v112, v84 row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v85 row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v86 row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v87 row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[84:87], %[xa] offset:144\n"
+        "s_waitcnt lgkmcnt(8)\n"
+        "v_fmac_f32_dpp %[acc], v112, v88 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v89 row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v90 row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v91 row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[88:91], %[xa] offset:160\n"
+        "s_waitcnt lgkmcnt(8)\n"
+        "v_fmac_f32_dpp %[acc], v112, v92 row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v93 row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v94 row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v112, v95 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[92:95], %[xa] offset:176\n"
+        "ds_read_b32 v112, %[vl] offset:128\n"
+        // iteration B: v113, slots v96..v111
+        "s_waitcnt lgkmcnt(8)\n"
+        "v_fmac_f32_dpp %[acc], v113, v96 row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v97 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v98 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v99 row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[96:99], %[xa] offset:192\n"
+        "s_waitcnt lgkmcnt(8)\n"
+        "v_fmac_f32_dpp %[acc], v113, v100 row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v101 row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v102 row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v103 row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[100:103], %[xa] offset:208\n"
+        "s_waitcnt lgkmcnt(8)\n"
+        "v_fmac_f32_dpp %[acc], v113, v104 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v105 row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v106 row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v107 row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[104:107], %[xa] offset:224\n"
+        "s_waitcnt lgkmcnt(8)\n"
+        "v_fmac_f32_dpp %[acc], v113, v108 row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v109 row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v110 row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v113, v111 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[108:111], %[xa] offset:240\n"
+        "ds_read_b32 v113, %[vl] offset:192\n"
+        "s_sub_u32 %[it], %[it], 1\n s_cmp_lg_u32 %[it], 0\n s_cbranch_scc1 1b\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [it] "+s"(it)
+        : [xa] "v"(xa), [vl] "v"(vl)
+        : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91",
+          "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102",
+          "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112",
+          "v113", "scc");
+    long long t1 = __builtin_amdgcn_s_memtime();
+    out[threadIdx.x] = acc;
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
+int main6() {
+    float *out;
+    long long *cyc, h;
+    (void)hipMalloc(&out, 1024 * 4);
+    (void)hipMalloc(&cyc, 8);
+    const int iters = 20000;  // x 32 nonzeros
+    for (int k = 0; k < 2; ++k)
+        hipLaunchKernelGGL(ring_XDPP, dim3(1), dim3(64), 0, 0, out, cyc, iters, 0.5f);
+    (void)hipMemcpy(&h, cyc, 8, hipMemcpyDeviceToHost);
+    printf("{\"case\": \"%s\", \"cycles_per_nonzero\": %.2f}\n",
+           "asm ring 8 batches: x b128, v by ds_read_b32 per 16 + DPP row_newbcast",
+           (double)h / (iters * 32.0));
+    return 0;
+}
+
 int main5() {
     float *out, *vals;
     long long *cyc, h;
@@ -995,7 +1106,7 @@ int main5() {
     printf("{\"case\": \"%s\", \"cycles_per_nonzero\": %.2f}\n",
            "x b128 half-ring + v by s_buffer_load_dwordx16 (3 banks, 2 ahead)",
            (double)h / (iters * 96.0));
-    return 0;
+    return main6();
 }
 
 int main4() {

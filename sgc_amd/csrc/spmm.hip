@@ -550,6 +550,15 @@ constexpr int kHubUnroll = 6;  // lcm(kHubDepth, 2): X ring slot and colv parity
 #ifndef SGC_HUB_PRE
 #define SGC_HUB_PRE (SGC_HUB_ASM ? 4 : 3)
 #endif
+#ifndef SGC_HUB_QUIET_SIMD
+// leave the chain wave's SIMD to it alone (waves w % 4 == 0 idle): measured
+// equal at HC = 32 and 14% slower at HC = 64 (shorter rounds), so the SIMD's
+// other waves are not what holds the chain back (profiles/r02/hub_probe_lib_*.log)
+#define SGC_HUB_QUIET_SIMD 0
+#endif
+#ifndef SGC_HUB_DPP
+#define SGC_HUB_DPP 1  // the asm chain's S values by DPP row broadcast (hub_chain_dpp)
+#endif
 constexpr int kHubPre = SGC_HUB_PRE;  // LDS batches of 4 nonzeros the chain reads ahead
 #ifndef SGC_HUB_SCHED
 #define SGC_HUB_SCHED 0
@@ -559,7 +568,10 @@ template <int HC, int NL>
 struct HubShape {
     static constexpr int kSegs = kWave / HC;                     // nonzero runs per loader wave
     static constexpr int kPerLoader = kHubInstr * kSegs;         // nonzeros per loader per round
-    static constexpr int kRound = NL * kPerLoader;               // nonzeros per round (240 / 480 at NL = 15)
+    // loader waves that load: all NL, or (SGC_HUB_QUIET_SIMD) all but the
+    // waves sharing the chain wave's SIMD (waves 4, 8, 12 of a 16-wave block)
+    static constexpr int kActive = SGC_HUB_QUIET_SIMD ? NL - NL / 4 : NL;
+    static constexpr int kRound = kActive * kPerLoader;          // nonzeros per round (240 / 480 at NL = 15)
     // chain read-ahead in batches of 4; HC = 64 fits at most 4 in 160 KB of LDS
     static constexpr int kPre = (HC == 64 && kHubPre > 4) ? 4 : kHubPre;
     static constexpr int kPad = 4 * kPre;                        // read-ahead past kRound
@@ -683,6 +695,146 @@ __device__ __forceinline__ void hub_chain_asm(float &acc, uint32_t xa, uint32_t 
 }
 #endif
 
+#if SGC_HUB_DPP
+// The chain with the S values off the LDS-read path: one ds_read_b32 per 16
+// nonzeros (lane l reads v[16i + (l & 15)], so each 16-lane row holds the
+// iteration's 16 values) and every FMA takes its S value by a DPP row
+// broadcast (v_fmac_f32_dpp ... row_newbcast:k): four LDS reads per 16
+// nonzeros instead of eight.  Same operands and order as hub_chain_asm:
+// acc = fma(v[k], x[k], acc).  X ring of four b128 slots (v80..v95) read four
+// batches ahead; S in v96 (even iterations) / v97 (odd), read two iterations
+// ahead (gv carries 32 floats of padding for it).  Invariant at the top of an
+// iteration: outstanding LDS reads = [S_i, X0..X3, S_i+1].
+__device__ __forceinline__ void hub_chain_dpp(float &acc, uint32_t xa, uint32_t vl, int iters,
+                                              int rem) {
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n"
+        "ds_read_b32 v96, %[vl]\n"
+        "ds_read_b128 v[80:83], %[xa]\n"
+        "ds_read_b128 v[84:87], %[xa] offset:16\n"
+        "ds_read_b128 v[88:91], %[xa] offset:32\n"
+        "ds_read_b128 v[92:95], %[xa] offset:48\n"
+        "ds_read_b32 v97, %[vl] offset:64\n"
+        "s_cmp_eq_u32 %[it], 0\n"
+        "s_cbranch_scc1 2f\n"
+        "1:\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32_dpp %[acc], v96, v80 row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v81 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v82 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v83 row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[80:83], %[xa] offset:64\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32_dpp %[acc], v96, v84 row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v85 row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v86 row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v87 row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[84:87], %[xa] offset:80\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32_dpp %[acc], v96, v88 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v89 row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v90 row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v91 row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[88:91], %[xa] offset:96\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32_dpp %[acc], v96, v92 row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v93 row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v94 row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v95 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[92:95], %[xa] offset:112\n"
+        "ds_read_b32 v96, %[vl] offset:128\n"
+        "v_add_u32 %[xa], 64, %[xa]\n"
+        "v_add_u32 %[vl], 64, %[vl]\n"
+        "s_sub_u32 %[it], %[it], 1\n"
+        "s_cmp_eq_u32 %[it], 0\n"
+        "s_cbranch_scc1 3f\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32_dpp %[acc], v97, v80 row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v81 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v82 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v83 row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[80:83], %[xa] offset:64\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32_dpp %[acc], v97, v84 row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v85 row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v86 row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v87 row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[84:87], %[xa] offset:80\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32_dpp %[acc], v97, v88 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v89 row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v90 row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v91 row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[88:91], %[xa] offset:96\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32_dpp %[acc], v97, v92 row_newbcast:12 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v93 row_newbcast:13 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v94 row_newbcast:14 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v95 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+        "ds_read_b128 v[92:95], %[xa] offset:112\n"
+        "ds_read_b32 v97, %[vl] offset:128\n"
+        "v_add_u32 %[xa], 64, %[xa]\n"
+        "v_add_u32 %[vl], 64, %[vl]\n"
+        "s_sub_u32 %[it], %[it], 1\n"
+        "s_cmp_lg_u32 %[it], 0\n"
+        "s_cbranch_scc1 1b\n"
+        // even count done: the next iteration's S is in v96
+        "2:\n"
+        "s_cmp_gt_u32 %[rem], 0\n"
+        "s_cbranch_scc0 5f\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32_dpp %[acc], v96, v80 row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v81 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v82 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v83 row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "s_cmp_gt_u32 %[rem], 1\n"
+        "s_cbranch_scc0 5f\n"
+        "s_waitcnt lgkmcnt(3)\n"
+        "v_fmac_f32_dpp %[acc], v96, v84 row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v85 row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v86 row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v87 row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "s_cmp_gt_u32 %[rem], 2\n"
+        "s_cbranch_scc0 5f\n"
+        "s_waitcnt lgkmcnt(2)\n"
+        "v_fmac_f32_dpp %[acc], v96, v88 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v89 row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v90 row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v96, v91 row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "s_branch 5f\n"
+        // odd count done: the next iteration's S is in v97
+        "3:\n"
+        "s_cmp_gt_u32 %[rem], 0\n"
+        "s_cbranch_scc0 5f\n"
+        "s_waitcnt lgkmcnt(4)\n"
+        "v_fmac_f32_dpp %[acc], v97, v80 row_newbcast:0 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v81 row_newbcast:1 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v82 row_newbcast:2 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v83 row_newbcast:3 row_mask:0xf bank_mask:0xf\n"
+        "s_cmp_gt_u32 %[rem], 1\n"
+        "s_cbranch_scc0 5f\n"
+        "s_waitcnt lgkmcnt(3)\n"
+        "v_fmac_f32_dpp %[acc], v97, v84 row_newbcast:4 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v85 row_newbcast:5 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v86 row_newbcast:6 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v87 row_newbcast:7 row_mask:0xf bank_mask:0xf\n"
+        "s_cmp_gt_u32 %[rem], 2\n"
+        "s_cbranch_scc0 5f\n"
+        "s_waitcnt lgkmcnt(2)\n"
+        "v_fmac_f32_dpp %[acc], v97, v88 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v89 row_newbcast:9 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v90 row_newbcast:10 row_mask:0xf bank_mask:0xf\n"
+        "v_fmac_f32_dpp %[acc], v97, v91 row_newbcast:11 row_mask:0xf bank_mask:0xf\n"
+        "s_branch 5f\n"
+        "5:\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        : [acc] "+v"(acc), [xa] "+v"(xa), [vl] "+v"(vl), [it] "+s"(iters)
+        : [rem] "s"(rem)
+        : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91",
+          "v92", "v93", "v94", "v95", "v96", "v97", "scc", "memory");
+}
+#endif
+
 // NL loader waves + the chain wave per workgroup: 15 (1024 threads, ~133 KB
 // of LDS: one workgroup per CU) or 7 (512 threads, ~68 KB: two per CU, half
 // the CU held per hub chain; sgc_set_tuning("hub_loaders")).
@@ -694,9 +846,14 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
     using Sh = HubShape<HC, NL>;
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) float gxT[2][HC * Sh::kStride];  // 2 x 66.5 KB
-    __shared__ __attribute__((aligned(16))) float gv[2][Sh::kRound + Sh::kPad];  // + read-ahead
+    __shared__ __attribute__((aligned(16)))
+    float gv[2][Sh::kRound + Sh::kPad + (SGC_HUB_DPP ? 32 : 0)];  // + read-ahead
     const int lane = threadIdx.x & (kWave - 1);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    // loader index li of wave w (waves sharing SIMD 0 with the chain wave idle
+    // under SGC_HUB_QUIET_SIMD); wave 0 runs the chain
+    const bool loader = w > 0 && (!SGC_HUB_QUIET_SIMD || (w & 3) != 0);
+    const int li = SGC_HUB_QUIET_SIMD ? w - 1 - w / 4 : w - 1;
     const int h = blockIdx.x / n_chunks;
     const int c = blockIdx.x - h * n_chunks;
     const int row = hub_rows[h];
@@ -718,11 +875,11 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
     // loads that use them (per-nonzero scalar loads, each waited on, cost
     // ~0.4 us per round: 493 -> 406 us on the 47,857-nonzero row).
     auto load_col = [&](int r, int p) {
-        const int kr = k0 + r * Sh::kRound + (w - 1) * Sh::kPerLoader;
+        const int kr = k0 + r * Sh::kRound + li * Sh::kPerLoader;
         colv[p] = col[min(kr + my_k, k1 - 1)];
     };
     auto load_x = [&](int r, int s, int p) {
-        const int kr = k0 + r * Sh::kRound + (w - 1) * Sh::kPerLoader;
+        const int kr = k0 + r * Sh::kRound + li * Sh::kPerLoader;
 #pragma unroll
         for (int j = 0; j < kHubInstr; ++j) {
             int cj = __builtin_amdgcn_readlane(colv[p], j);
@@ -736,16 +893,16 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
     };
     auto store = [&](int buf, int s) {
         f4 *dst = reinterpret_cast<f4 *>(
-            &gxT[buf][fl * Sh::kStride + (w - 1) * Sh::kPerLoader + seg * kHubInstr]);
+            &gxT[buf][fl * Sh::kStride + li * Sh::kPerLoader + seg * kHubInstr]);
 #pragma unroll
         for (int q = 0; q < kHubInstr / 4; ++q)
             dst[q] = f4{regs[s][4 * q], regs[s][4 * q + 1], regs[s][4 * q + 2], regs[s][4 * q + 3]};
-        if (lane < Sh::kPerLoader) gv[buf][(w - 1) * Sh::kPerLoader + lane] = vreg[s];
+        if (lane < Sh::kPerLoader) gv[buf][li * Sh::kPerLoader + lane] = vreg[s];
     };
     // Loads are never predicated (rounds past the row re-read its last
     // nonzero): a conditional load makes its registers a phi, and copying a
     // phi waits for every load in flight.
-    if (w > 0) {
+    if (loader) {
 #pragma unroll
         for (int s = 0; s < kHubDepth; ++s) {
             load_col(s, s & 1);
@@ -778,7 +935,7 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
 #define SGC_HUB_EXPERIMENT 0  // timing probes only: 1 = no FMA chain, 2 = no X loads
 #endif
             if (w == 0) HUB_STAMP(0, r);
-            if (w > 0) {
+            if (loader) {
                 if (r + 1 < n_round) store(buf ^ 1, (s + 1) % kHubDepth);
                 if (w == 1) HUB_STAMP(2, r);
                 // ids of round r+D+1 first, so waiting for them (next round)
@@ -787,7 +944,7 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
                     load_col(r + kHubDepth + 1, (s + kHubDepth + 1) & 1);
                     load_x(r + kHubDepth, s % kHubDepth, (s + kHubDepth) & 1);
                 }
-            } else if (SGC_HUB_EXPERIMENT != 1) {
+            } else if (w == 0 && SGC_HUB_EXPERIMENT != 1) {
                 const int n = min(Sh::kRound, k1 - (k0 + r * Sh::kRound));
                 const int n4 = n >> 2;
                 // LDS reads run kPre batches of four nonzeros ahead of the FMA
@@ -807,13 +964,23 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
                 // alone however deep the ring, vs ~5 for the bare dependent
                 // FMA), ~15 cycles per nonzero beside the loaders' LDS writes
                 // (per-round clock stamps: the chain loop is 95% of each
-                // round; profiles/r02/hub_stamps_*.log).
+                // round; profiles/r02/hub_stamps_*.log).  hub_chain_dpp (the
+                // default) halves the chain's LDS reads -- S by DPP row
+                // broadcast: 9.5 cycles per nonzero alone, and the
+                // 47,857-nonzero row 341 -> 325 us (HC = 64), 306 -> 281 us
+                // (HC = 32), profiles/r02/hub_probe_{base_v2,lib_hubdpp}.log.
                 static_assert(kPre >= 4, "the asm chain reads 4 batches ahead");
                 typedef __attribute__((address_space(3))) const float lds_f;
                 uint32_t xa = (uint32_t)(size_t)(lds_f *)(&gxT[buf][fl * Sh::kStride]);
                 uint32_t va = (uint32_t)(size_t)(lds_f *)(&gv[buf][0]);
                 const int iters = n4 >> 2, rem = n4 & 3;
+#if SGC_HUB_DPP
+                (void)va;
+                const uint32_t vl = (uint32_t)(size_t)(lds_f *)(&gv[buf][lane & 15]);
+                hub_chain_dpp(acc, xa, vl, iters, rem);
+#else
                 hub_chain_asm(acc, xa, va, iters, rem);
+#endif
 #elif SGC_HUB_SCHED
                 const f4 *xs = reinterpret_cast<const f4 *>(&gxT[buf][fl * Sh::kStride]);
                 const f4 *vs = reinterpret_cast<const f4 *>(&gv[buf][0]);

@@ -22,7 +22,12 @@ from . import _lib
 # bound is the tail -- one wave walking a long row with ~16 nonzeros in flight
 # -- against the launch's duration (nnz x F bytes):
 #   heavy = nnz*F / 2^23 to the nearest power of two, clamped to [64, 512];
-#   hub   = max(heavy, nnz / 1024, 256).
+#   hub   = max(heavy, nnz / 1024, 256), capped at 8,192 below 16 M nonzeros.
+# The cap (round 2): half of Reddit (11.7 M nonzeros, a P = 2 rank) with
+# nnz / 1024 = 11.4k leaves its ~11.5k-nonzero rows as one-wave heavy items
+# whose latency outlasts the rank's slice passes -- 2.66 ms per hop vs 2.43
+# with hubs above 8,192 (96 rows); the whole graph (19 vs 172 hubs) and a
+# quarter (52 either way) are unchanged (profiles/r02/p24_hub_sweep.log).
 # Measured (scripts/sweep_narrow.py, profiles/r01_heavy_threshold_sweep.log,
 # r01_rank_work_threshold_sweep.log): Reddit full graph 512 / ~10 hubs (988
 # hubs cost +20%); a 1/8 row block 128-256 / its 132 rows above 2,048
@@ -34,6 +39,7 @@ DEFAULT_HEAVY_THRESHOLD = int(_HEAVY_ENV) if _HEAVY_ENV else None
 _HUB_ENV = os.environ.get("SGC_AMD_HUB_THRESHOLD")
 DEFAULT_HUB_THRESHOLD = int(_HUB_ENV) if _HUB_ENV else None
 HUB_SHARE = 1024
+HUB_CAP, HUB_CAP_BELOW_NNZ = 8192, 1 << 24
 
 
 def auto_heavy_threshold(nnz_range, width):
@@ -43,7 +49,10 @@ def auto_heavy_threshold(nnz_range, width):
 
 
 def auto_hub_threshold(nnz_range, heavy_threshold):
-    return max(int(heavy_threshold), int(nnz_range) // HUB_SHARE, 256)
+    hub = int(nnz_range) // HUB_SHARE
+    if int(nnz_range) < HUB_CAP_BELOW_NNZ:
+        hub = min(hub, HUB_CAP)
+    return max(int(heavy_threshold), hub, 256)
 
 
 class Plan(NamedTuple):
