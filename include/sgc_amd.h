@@ -227,9 +227,16 @@ int sgc_timing_collect(float *light_ms_host, float *hub_ms_host, int64_t capacit
  * SGC_SPMM_HUB_SERIAL: run the hub rows' kernel on `stream` before the light
  * kernel instead of beside it on a side stream (no fork/join events); for
  * launches whose longest hub chain is shorter than the ~20-30 us a
- * cross-stream fork/join costs (sgc_set_tuning "hub_stream" overrides). */
+ * cross-stream fork/join costs (sgc_set_tuning "hub_stream" overrides).
+ * SGC_SPMM_LIGHT_ORDER: `plan` holds row_end - row_begin entries: its n_heavy
+ * heavy rows (as sgc_plan_build writes them) followed by every other row of
+ * the range, in the order the light rows are to be processed (the Python
+ * layer sorts them by length, so the rows sharing a wavefront in the
+ * multi-row kernel have about the same length and few lanes idle-load past
+ * their row's end).  A schedule only: results never depend on it. */
 enum { SGC_SPMM_X_PADDED = 1, SGC_SPMM_Y_PADDED = 2, SGC_SPMM_NO_HUB = 4,
-       SGC_SPMM_HUB_ONLY = 8, SGC_SPMM_ACCUMULATE = 16, SGC_SPMM_HUB_SERIAL = 32 };
+       SGC_SPMM_HUB_ONLY = 8, SGC_SPMM_ACCUMULATE = 16, SGC_SPMM_HUB_SERIAL = 32,
+       SGC_SPMM_LIGHT_ORDER = 64 };
 int sgc_spmm_csr_f32_ex(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                         int64_t row_begin, int64_t row_end,
                         const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,

@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
     int row_begin, int n_rows, int F, int F_load, int LR, int vec_store, int n_sub,
     const int *__restrict__ heavy_rows, int n_heavy, int heavy_threshold, int accum,
-    int heavy_packed) {
+    int heavy_packed, const int *__restrict__ light_rows) {
     constexpr int V = 4, U = kRowsU < LB / 2 ? kRowsU : LB / 2;
     constexpr int kSteps = LB / U;  // steps per LDS block
     static_assert(kSteps >= 2 && kSteps % 2 == 0, "bad block");
@@ -393,6 +393,17 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
         const int hi = wave * R + sub;
         if (sub < R && hi < n_heavy) {
             const int row = heavy_rows[hi];
+            r = row - row_begin;
+            k0 = row_ptr[row];
+            len = row_ptr[row + 1] - k0;
+            mine = true;
+        }
+    } else if (light_rows) {  // light rows in the plan's order (n_rows of them here)
+        const int w = wave - n_heavy_items;
+        if (w * R >= n_rows) return;  // wave-uniform
+        const int li = w * R + sub;
+        if (sub < R && li < n_rows) {
+            const int row = light_rows[li];
             r = row - row_begin;
             k0 = row_ptr[row];
             len = row_ptr[row + 1] - k0;
@@ -1088,6 +1099,8 @@ struct LaunchArgs {
     int slices;
     int accum;
     hipStream_t stream;
+    const int *light_rows;  // SGC_SPMM_LIGHT_ORDER: the light rows in processing order, or null
+    int n_light;
 };
 
 // A side stream + fork/join events per (device, priority) for the hub kernel
@@ -1225,13 +1238,16 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int n_sub = slices > 1 ? SW / (kWave * VH) : (F_load + kWave * VH - 1) / (kWave * VH);
     const int64_t heavy_waves = g_heavy_packed ? ((int64_t)a.n_heavy + R - 1) / R
                                                : (int64_t)a.n_heavy * n_sub;
-    const int64_t waves = heavy_waves + (a.n_rows + R - 1) / R;
+    // light items: every row (non-light rows skip themselves), or with a
+    // light order exactly the light rows
+    const int n_light_items = a.light_rows ? a.n_light : a.n_rows;
+    const int64_t waves = heavy_waves + (n_light_items + R - 1) / R;
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     dim3 grid((unsigned)blocks, (unsigned)slices);
     hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, SGC_HEAVY_U>), grid, dim3(kBlock), g_light_lds,
                        a.stream, a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
-                       a.n_rows, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
-                       a.heavy_threshold, a.accum, g_heavy_packed);
+                       n_light_items, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
+                       a.heavy_threshold, a.accum, g_heavy_packed, a.light_rows);
     return hipGetLastError();
 }
 
@@ -1364,6 +1380,15 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     SGC_REQUIRE(n_heavy >= 0 && (n_heavy == 0 || heavy_rows), SGC_EINVAL, "spmm: bad plan");
     const int64_t n_rows = row_end - row_begin;
     if (n_rows == 0) return SGC_OK;
+    // SGC_SPMM_LIGHT_ORDER: plan = [n_heavy heavy rows | the other rows in
+    // processing order] (taken before the hub split below moves heavy_rows)
+    const int *light_rows = nullptr;
+    int64_t n_light = 0;
+    if ((flags & SGC_SPMM_LIGHT_ORDER) && heavy_rows) {
+        SGC_REQUIRE(n_heavy <= n_rows, SGC_EINVAL, "spmm: light order with n_heavy > rows");
+        light_rows = heavy_rows + n_heavy;
+        n_light = n_rows - n_heavy;
+    }
     if (!heavy_rows) {
         n_heavy = 0;
         heavy_threshold = INT32_MAX;  // no plan: every row is a light item
@@ -1440,6 +1465,8 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
 
     LaunchArgs a{row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)n_rows, (int)F,
                  heavy_rows, (int)n_heavy, heavy_threshold, 0, accum, light_stream};
+    a.light_rows = light_rows;  // used by the multi-row kernel (the one-row kernel: natural order)
+    a.n_light = (int)n_light;
     // 16-B lanes over F rounded up to 4 columns: X rows must be 16-B aligned
     // and readable that far (flag SGC_SPMM_X_PADDED unless F % 4 == 0)
     const int64_t F4 = (F + 3) / 4 * 4;

@@ -61,10 +61,14 @@ class Plan(NamedTuple):
     n_hub: int
     threshold: int
     max_hub_degree: int = 0  # nonzeros of the longest hub row (0: no hub rows)
+    ordered: bool = False  # rows also lists the light rows, longest first (SPMM_LIGHT_ORDER)
 
     def hub_flags(self):
-        """SPMM_HUB_SERIAL when the hub kernel is short enough to run in line."""
-        return SPMM_HUB_SERIAL if 0 < self.max_hub_degree <= HUB_SERIAL_MAX_DEGREE else 0
+        """The plan's launch flags: SPMM_HUB_SERIAL when the hub kernel is
+        short enough to run in line, SPMM_LIGHT_ORDER when `rows` carries the
+        light rows' order."""
+        f = SPMM_HUB_SERIAL if 0 < self.max_hub_degree <= HUB_SERIAL_MAX_DEGREE else 0
+        return f | (SPMM_LIGHT_ORDER if self.ordered else 0)
 
 
 NO_PLAN = Plan(None, 0, 0, 0)
@@ -75,6 +79,13 @@ SPMM_NO_HUB = 4    # split launch: every row but the plan's hub rows
 SPMM_HUB_ONLY = 8  # split launch: only the hub rows, on the current stream
 SPMM_ACCUMULATE = 16  # column-block pass: continue the chains stored in out
 SPMM_HUB_SERIAL = 32  # hub kernel before the light kernel on the same stream
+SPMM_LIGHT_ORDER = 64  # plan rows = heavy rows + the light rows in processing order
+# Light rows of the multi-row kernel in length order (longest first), so the
+# rows sharing a wavefront have about the same length: a wave runs to its
+# longest row and the other rows' lanes re-load their last nonzero meanwhile
+# (the texture-address unit is ~86% busy on the Reddit hop, so those loads
+# cost time, profiles/r02/diag).  SGC_AMD_LIGHT_ORDER=0 keeps row order.
+LIGHT_ORDER = os.environ.get("SGC_AMD_LIGHT_ORDER", "1") != "0"
 # Longest hub row (nonzeros) for which the serial hub launch beats the
 # side-stream fork/join: its chain (~6.4 ns per nonzero) plus a
 # launch stays under the ~25 us the two cross-stream events cost.
@@ -265,7 +276,15 @@ class DeviceCSR:
                 r = int(buf[0].item())
                 ends = self.row_ptr[[r, r + 1]].tolist()
                 deg = ends[1] - ends[0]
-            self._plans[key] = Plan(buf[:max(h, 1)].clone(), h, nh, threshold, deg)
+            rows, ordered = buf[:max(h, 1)].clone(), False
+            if LIGHT_ORDER and self.device.type == "cuda" and n > h:
+                rp = self.row_ptr.to(torch.int64)
+                d = rp[row_begin + 1:row_end + 1] - rp[row_begin:row_end]
+                light = torch.nonzero(d <= threshold).squeeze(1)
+                by_len = torch.sort(d[light], descending=True, stable=True).indices
+                rows = torch.cat([buf[:h], (light[by_len] + row_begin).to(torch.int32)])
+                ordered = True
+            self._plans[key] = Plan(rows, h, nh, threshold, deg, ordered)
         return self._plans[key]
 
 
