@@ -175,6 +175,15 @@ int sgc_plan_build(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
                    int32_t heavy_threshold, int32_t hub_threshold, int32_t *plan,
                    int64_t plan_capacity, int64_t *n_heavy_host, int64_t *n_hub_host,
                    void *stream);
+/* The light rows' processing order for SGC_SPMM_LIGHT_ORDER: every row of
+ * [row_begin, row_end) with at most heavy_threshold nonzeros, longest first,
+ * ties in row order (a stable counting sort on the host after one read-back
+ * of row_ptr), written to light[0 .. *n_light_host) on the device (light
+ * must hold row_end - row_begin words); synchronous on `stream`.  Place it
+ * after the n_heavy rows of sgc_plan_build's plan.  A schedule only. */
+int sgc_plan_light_order(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
+                         int32_t heavy_threshold, int32_t *light, int64_t *n_light_host,
+                         void *stream);
 
 /* ---------------------------------------------------------------------------
  * One hop Y = S[row_begin:row_end, :] . X  (utils.py:95, torch.spmm).

@@ -41,6 +41,7 @@ SIGNATURES = {
     "sgc_plan_capacity": (_i64, [_i64]),
     "sgc_plan_build": (ctypes.c_int, [_p, _i64, _i64, _i32, _i32, _p, _i64, ctypes.POINTER(_i64),
                                       ctypes.POINTER(_i64), _p]),
+    "sgc_plan_light_order": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, ctypes.POINTER(_i64), _p]),
     "sgc_spmm_csr_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
                                         _p, _i64, _i64, _i32, _p]),
     "sgc_spmm_csr_f32_ex": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,

@@ -26,6 +26,8 @@ int csr64_to_csr(const int64_t *crow, const int64_t *col, const float *vals, int
 int build_plan(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int32_t threshold,
                int32_t hub_threshold, int32_t *plan, int64_t capacity, int64_t *n_heavy_host,
                int64_t *n_hub_host, hipStream_t stream);
+int light_order(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int32_t threshold,
+                int32_t *light, int64_t *n_light_host, hipStream_t stream);
 int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                 int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
                 int64_t ldy, int64_t F, const int32_t *heavy_rows, int64_t n_heavy,
@@ -154,6 +156,13 @@ int sgc_csr_to_coo64(const int32_t *row_ptr, const int32_t *col_idx, int64_t n_r
 }
 
 int64_t sgc_plan_capacity(int64_t n_rows) { return 2 * (n_rows < 0 ? 0 : n_rows) + 1; }
+
+int sgc_plan_light_order(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
+                         int32_t heavy_threshold, int32_t *light, int64_t *n_light_host,
+                         void *stream) {
+    return light_order(row_ptr, row_begin, row_end, heavy_threshold, light, n_light_host,
+                       as_stream(stream));
+}
 
 int sgc_plan_build(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
                    int32_t heavy_threshold, int32_t hub_threshold, int32_t *plan,

@@ -278,11 +278,17 @@ class DeviceCSR:
                 deg = ends[1] - ends[0]
             rows, ordered = buf[:max(h, 1)].clone(), False
             if LIGHT_ORDER and self.device.type == "cuda" and n > h:
-                rp = self.row_ptr.to(torch.int64)
-                d = rp[row_begin + 1:row_end + 1] - rp[row_begin:row_end]
-                light = torch.nonzero(d <= threshold).squeeze(1)
-                by_len = torch.sort(d[light], descending=True, stable=True).indices
-                rows = torch.cat([buf[:h], (light[by_len] + row_begin).to(torch.int32)])
+                # plan rows = [heavy rows | light rows longest first]
+                rows = torch.empty(n, dtype=torch.int32, device=self.device)
+                rows[:h].copy_(buf[:h])
+                n_light = _lib._i64(0)
+                with torch.cuda.device(self.device):
+                    _lib.check(lib.sgc_plan_light_order(
+                        _lib.ptr(self.row_ptr), row_begin, row_end, threshold,
+                        _lib.ptr(rows[h:]), ctypes_byref(n_light),
+                        _lib.stream_handle(self.device)), "plan_light_order")
+                if int(n_light.value) != n - h:
+                    raise RuntimeError("sgc_amd: light order does not cover the light rows")
                 ordered = True
             self._plans[key] = Plan(rows, h, nh, threshold, deg, ordered)
         return self._plans[key]

@@ -571,3 +571,25 @@ def test_graphed_propagation_bit_exact(tiny_cases, name, K, hub):
     assert bits_equal(out2.cpu().numpy(), want2)
     with pytest.raises(RuntimeError):
         g.run(X[:, :1].contiguous())
+
+
+@pytest.mark.parametrize("r0,r1,th", [(0, 4000, 7), (123, 3001, 0), (0, 4000, 2**31 - 1), (50, 50, 5)])
+def test_plan_light_order(r0, r1, th):
+    """sgc_plan_light_order: the light rows (degree <= threshold) of the range,
+    longest first, ties in row order -- as a stable sort on the host."""
+    import ctypes
+    from sgc_amd import _lib
+    rng = np.random.default_rng(r0 + r1 + th)
+    deg = rng.integers(0, 20, 4000)
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    rp_d = torch.from_numpy(rp).to(DEV)
+    out = torch.full((max(1, r1 - r0),), -1, dtype=torch.int32, device=DEV)
+    n = ctypes.c_int64(-1)
+    lib = _lib.load()
+    _lib.check(lib.sgc_plan_light_order(_lib.ptr(rp_d), r0, r1, th, _lib.ptr(out), ctypes.byref(n),
+                                        _lib.stream_handle(DEV)), "plan_light_order")
+    d = deg[r0:r1]
+    light = np.flatnonzero(d <= th)
+    want = (light[np.argsort(-d[light], kind="stable")] + r0).astype(np.int32)
+    assert n.value == len(want)
+    assert np.array_equal(out[:n.value].cpu().numpy(), want)
