@@ -1693,7 +1693,7 @@ int build_plan(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
 
 // Light rows (degree <= threshold) longest first, ties in row order: a
 // stable counting sort over the degrees on the host (one read-back of the
-// range's row_ptr; ~1 ms at Reddit shape).
+// range's row_ptr through a pinned buffer; ~1 ms at Reddit shape).
 int light_order(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int32_t threshold,
                 int32_t *light, int64_t *n_light_host, hipStream_t stream) {
     SGC_REQUIRE(row_ptr && light && n_light_host, SGC_EINVAL, "light_order: null pointer");
@@ -1702,8 +1702,22 @@ int light_order(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int3
                 "light_order: bad row range or threshold");
     *n_light_host = 0;
     if (n_rows == 0) return SGC_OK;
-    std::vector<int32_t> rp((size_t)n_rows + 1);
-    SGC_HIP_CHECK(hipMemcpyAsync(rp.data(), row_ptr + row_begin, rp.size() * sizeof(int32_t),
+    // pinned staging, kept for the process (grown on demand): a first large
+    // pageable device-to-host copy costs the runtime tens of ms
+    static std::mutex mu;
+    static int32_t *pinned = nullptr;
+    static size_t pinned_words = 0;
+    std::lock_guard<std::mutex> lock(mu);
+    const size_t need = 2 * ((size_t)n_rows + 1);  // row_ptr in, order out
+    if (pinned_words < need) {
+        if (pinned) SGC_HIP_CHECK(hipHostFree(pinned));
+        pinned = nullptr;
+        pinned_words = 0;
+        SGC_HIP_CHECK(hipHostMalloc((void **)&pinned, need * sizeof(int32_t), hipHostMallocDefault));
+        pinned_words = need;
+    }
+    int32_t *rp = pinned;
+    SGC_HIP_CHECK(hipMemcpyAsync(rp, row_ptr + row_begin, ((size_t)n_rows + 1) * sizeof(int32_t),
                                  hipMemcpyDeviceToHost, stream));
     SGC_HIP_CHECK(hipStreamSynchronize(stream));
     // buckets up to the longest light row, not the threshold (which may be
@@ -1720,13 +1734,13 @@ int light_order(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int3
     }
     for (size_t t = 1; t < start.size(); ++t) start[t] += start[t - 1];
     const int64_t n_light = start.back();
-    std::vector<int32_t> out((size_t)std::max<int64_t>(1, n_light));
+    int32_t *out = pinned + n_rows + 1;
     for (int64_t i = 0; i < n_rows; ++i) {
         const int64_t d = (int64_t)rp[i + 1] - rp[i];
         if (d <= threshold) out[(size_t)start[(size_t)(top - d)]++] = (int32_t)(row_begin + i);
     }
     if (n_light > 0) {
-        SGC_HIP_CHECK(hipMemcpyAsync(light, out.data(), (size_t)n_light * sizeof(int32_t),
+        SGC_HIP_CHECK(hipMemcpyAsync(light, out, (size_t)n_light * sizeof(int32_t),
                                      hipMemcpyHostToDevice, stream));
         SGC_HIP_CHECK(hipStreamSynchronize(stream));
     }
