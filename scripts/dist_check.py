@@ -31,7 +31,7 @@ from sgc_amd.distributed import RowPartitionedPropagator, TiledPropagator, make_
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="reddit")
-    ap.add_argument("--partition", default="rows", choices=["rows", "tiles", "cyclic"])
+    ap.add_argument("--partition", default="rows", choices=["rows", "tiles", "cyclic", "features"])
     ap.add_argument("--groups", type=int, default=4, help="cyclic: column groups")
     ap.add_argument("--tile", type=int, default=64, help="cyclic: rows per tile")
     ap.add_argument("--col-blocks", type=int, default=2)
@@ -78,6 +78,15 @@ def main():
         mine = cp.propagate(X, K, output="sharded")
         row_index = cp.row_index
         r0, r1 = 0, 0
+    elif args.partition == "features":
+        from sgc_amd.distributed import FeaturePartitionedPropagator, equal_row_bounds
+        from sgc_amd.propagate import DeviceCSR
+        csr = DeviceCSR.from_host_arrays(np.asarray(S.row_ptr), np.asarray(S.col_idx),
+                                         np.asarray(S.val), device=dev)
+        fp = FeaturePartitionedPropagator(csr, host_staging=True)
+        mine = fp.propagate(X, K, output="sharded")
+        rb = equal_row_bounds(g["n"], world)
+        r0, r1 = int(rb[rank]), int(rb[rank + 1])
     elif args.partition == "tiles":
         tp = TiledPropagator(S.row_ptr, S.col_idx, S.val, rank, world, args.col_blocks, dev,
                              group_floats=args.group_floats, host_staging=True)
