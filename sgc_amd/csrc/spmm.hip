@@ -1162,6 +1162,10 @@ static bool g_timing = false;
 static std::vector<TimedLaunch> g_timed;
 static std::vector<hipEvent_t> g_event_pool;
 
+// Launches recorded but not yet collected are capped: timing left on without
+// sgc_timing_collect() stops recording instead of growing without bound.
+constexpr size_t kMaxTimed = 1 << 16;
+
 hipError_t pooled_event(hipEvent_t *e) {
     if (!g_event_pool.empty()) {
         *e = g_event_pool.back();
@@ -1170,6 +1174,39 @@ hipError_t pooled_event(hipEvent_t *e) {
     }
     return hipEventCreate(e);
 }
+
+// Error-path guards of launch_spmm (called with g_timing_mu held while a
+// TimedLaunch is filled): once the hub fork is recorded, the caller's stream
+// is always joined to the side stream, and pooled timing events that never
+// reached g_timed go back to the pool.
+struct SideJoin {
+    SideStream *side = nullptr;
+    hipStream_t stream = nullptr;
+    ~SideJoin() {
+        if (!side) return;
+        (void)hipEventRecord(side->join, side->s);
+        (void)hipStreamWaitEvent(stream, side->join, 0);
+    }
+    hipError_t join() {  // the normal path: report the join's own errors
+        SideStream *s = side;
+        side = nullptr;
+        hipError_t e = hipEventRecord(s->join, s->s);
+        return e != hipSuccess ? e : hipStreamWaitEvent(stream, s->join, 0);
+    }
+};
+
+struct TimedGuard {
+    TimedLaunch *tl = nullptr;  // non-null while its events are not in g_timed
+    ~TimedGuard() {
+        if (!tl) return;
+        for (hipEvent_t ev : {tl->l0, tl->l1, tl->h0, tl->h1})
+            if (ev) g_event_pool.push_back(ev);
+    }
+    void commit() {
+        g_timed.push_back(*tl);
+        tl = nullptr;
+    }
+};
 
 // Nonzeros per step: light items keep U*C*V <= ~40 registers of gathered X
 // per step; heavy sub-chunk items go deeper (UH).  The pipelined loop holds
@@ -1406,8 +1443,13 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     std::unique_lock<std::mutex> side_lock;
     std::unique_lock<std::mutex> timing_lock(g_timing_mu);
     TimedLaunch tl;
-    const bool timing = g_timing;
+    const bool timing = g_timing && g_timed.size() < kMaxTimed;
     if (!timing) timing_lock.unlock();
+    // declared after the locks: destroyed (join, events back to the pool)
+    // while they are still held
+    TimedGuard timed_guard;
+    if (timing) timed_guard.tl = &tl;
+    SideJoin side_join;
     hipStream_t light_stream = stream;
     if (n_hub > 0) {
         // hub rows (the heaviest n_hub of the plan) run on the side stream
@@ -1426,6 +1468,8 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             side_lock = std::unique_lock<std::mutex>(side->mu);
             SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
             SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
+            side_join.side = side;  // from here on every exit joins
+            side_join.stream = stream;
             hs = g_hub_first ? stream : side->s;
             light_stream = g_hub_first ? side->s : stream;
         }
@@ -1457,7 +1501,7 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
                 SGC_HIP_CHECK(pooled_event(&tl.l1));
                 SGC_HIP_CHECK(hipEventRecord(tl.l0, hs));
                 SGC_HIP_CHECK(hipEventRecord(tl.l1, hs));
-                g_timed.push_back(tl);
+                timed_guard.commit();
             }
             return SGC_OK;
         }
@@ -1544,12 +1588,9 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "spmm launch failed: %s", hipGetErrorString(e));
     if (timing) {
         SGC_HIP_CHECK(hipEventRecord(tl.l1, light_stream));
-        g_timed.push_back(tl);
+        timed_guard.commit();
     }
-    if (side) {  // join: the caller's stream waits for the hub kernel
-        SGC_HIP_CHECK(hipEventRecord(side->join, side->s));
-        SGC_HIP_CHECK(hipStreamWaitEvent(stream, side->join, 0));
-    }
+    if (side) SGC_HIP_CHECK(side_join.join());  // the caller's stream waits for the hub kernel
     return SGC_OK;
 }
 

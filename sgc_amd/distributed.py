@@ -63,6 +63,31 @@ def partition_bounds(row_ptr, world_size, balance="nnz"):
     raise ValueError(f"balance must be 'nnz' or 'rows', not {balance!r}")
 
 
+class _StreamDone:
+    """A finished-copy handle with the interface of an async collective's
+    work object: wait() makes the CURRENT stream wait for the work enqueued on
+    `stream` so far (like RCCL's Work.wait())."""
+    __slots__ = ("ev", "dev")
+
+    def __init__(self, stream):
+        self.dev = stream.device
+        self.ev = torch.cuda.Event()
+        self.ev.record(stream)
+
+    def wait(self):
+        torch.cuda.current_stream(self.dev).wait_event(self.ev)
+
+
+def _local_copy(full, loc):
+    """The all-gather of a one-rank group: a copy on the current stream --
+    which may be a comm stream, so on the GPU it returns a handle whose wait()
+    orders the consumer's stream after the copy (None on the CPU)."""
+    full.copy_(loc)
+    if full.is_cuda:
+        return _StreamDone(torch.cuda.current_stream(full.device))
+    return None
+
+
 def gathered_index(bounds, B, j):
     """Row of global node j in the gathered [P*B, F] exchange buffer: block p
     = the rank owning j lands at rows [p*B, p*B + rows_p)."""
@@ -194,7 +219,8 @@ def _default_spmm(shard: ShardCSR, X, out, layout="input", part="all", rows=None
     if fn is None:
         if len(launches) > 256:
             launches.clear()
-        fn = launches[key] = SpmmLaunch(csr, X, out, r0, r1, flags)
+        # keyed by the live tensors' pointers and geometry: no reference kept
+        fn = launches[key] = SpmmLaunch(csr, X, out, r0, r1, flags, keep_tensors=False)
     fn(_lib.stream_handle(X.device))
     return out
 
@@ -255,8 +281,7 @@ class RowPartitionedPropagator:
 
     def _all_gather(self, full, loc):
         if self.shard.world_size == 1:  # the exchange of one rank is a copy
-            full.copy_(loc)
-            return None
+            return _local_copy(full, loc)
         if not self.host_staging:
             return dist.all_gather_into_tensor(full, loc, group=self.group, async_op=True)
         h_full = torch.empty(full.shape, dtype=full.dtype)
@@ -662,11 +687,15 @@ def _pad_columns_allocated(t):
     return end * t.element_size() <= t.untyped_storage().nbytes()
 
 
-def _cyclic_spmm(csr, X, out, rows, accumulate, part="all", thresholds=(None, None)):
+def _cyclic_spmm(csr, X, out, rows, accumulate, part="all", thresholds=(None, None),
+                 own=(False, False)):
     """Rows [r0, r1) of csr . X into out[r0:r1] through the product engine;
     accumulate = continue the chains stored in out (SPMM_ACCUMULATE); part =
     "all", or the split launch "light" (all but the hub rows) / "hub";
-    thresholds = (heavy, hub) row-length thresholds of the plan."""
+    thresholds = (heavy, hub) row-length thresholds of the plan; own = (X, out)
+    are the propagator's own 128-B-row buffers, whose pad columns the kernel
+    may read / overwrite (never a caller's tensor: a column view of a wider
+    caller buffer would get its neighbouring columns clobbered)."""
     from . import _lib
     from .propagate import (SPMM_ACCUMULATE, SPMM_HUB_ONLY, SPMM_NO_HUB, SPMM_X_PADDED,
                             SPMM_Y_PADDED, SpmmLaunch, spmm)
@@ -680,9 +709,9 @@ def _cyclic_spmm(csr, X, out, rows, accumulate, part="all", thresholds=(None, No
         return spmm(csr, X, r0, r1, out=out[r0:r1], flags=flags, threshold=th, hub_threshold=hub)
     # the engine's own buffers have 128-B rows: let the kernel use 16-B lanes
     # (columns [F, round4(F)) of every row allocated; their values unused)
-    if _pad_columns_allocated(X):
+    if own[0] and _pad_columns_allocated(X):
         flags |= SPMM_X_PADDED
-    if _pad_columns_allocated(out):
+    if own[1] and _pad_columns_allocated(out):
         flags |= SPMM_Y_PADDED
     launches = csr.__dict__.setdefault("_launches", {})
     key = (r0, r1, flags, th, hub, X.data_ptr(), tuple(X.shape), X.stride(0), out.data_ptr(),
@@ -691,8 +720,10 @@ def _cyclic_spmm(csr, X, out, rows, accumulate, part="all", thresholds=(None, No
     if fn is None:
         if len(launches) > 256:
             launches.clear()
+        # keyed by the live tensors' pointers and geometry, so the entry holds
+        # no reference to them (a caller's X0 / out is never pinned)
         fn = launches[key] = SpmmLaunch(csr, X, out[r0:r1], r0, r1, flags, threshold=th,
-                                        hub_threshold=hub)
+                                        hub_threshold=hub, keep_tensors=False)
     fn(_lib.stream_handle(X.device))
     return out
 
@@ -731,7 +762,7 @@ class CyclicRowPropagator:
     output="sharded": this rank's rows of X_K, in ascending global order,
     global ids in `row_index` (valid rows only).  output="replicated": X_K
     [N, F] on every rank.  spmm_fn(csr, X, out, rows, accumulate, part,
-    thresholds) computes out[rows] (default: the HIP engine on ROCm tensors, the CPU twin
+    thresholds, own=(X is ours, out is ours)) computes out[rows] (default: the HIP engine on ROCm tensors, the CPU twin
     on CPU tensors).
 
     Heavy/hub row thresholds come from the rank's whole CSR (its nonzeros and
@@ -777,8 +808,7 @@ class CyclicRowPropagator:
 
     def _all_gather(self, full, loc):
         if self.shard.world_size == 1:
-            full.copy_(loc)
-            return None
+            return _local_copy(full, loc)
         if not self.host_staging:
             return dist.all_gather_into_tensor(full, loc, group=self.group, async_op=True)
         h = torch.empty(full.shape, dtype=full.dtype)
@@ -818,7 +848,7 @@ class CyclicRowPropagator:
             hub = auto_hub_threshold(self.shard.nnz, th)
         return int(th), int(max(hub, th))
 
-    def _hub_first(self, csr, X, out, chunks, h):
+    def _hub_first(self, csr, X, out, chunks, h, own):
         """Hop 1's hub rows, issued before any of its light chunks: one
         HUB_ONLY launch per row chunk on the hub stream (after the work already
         on the current stream), so their CU-sized workgroups are placed before
@@ -830,7 +860,7 @@ class CyclicRowPropagator:
         done = []
         with torch.cuda.stream(self._hub):
             for c, rows in enumerate(chunks):
-                self.spmm_fn(csr, X, out, rows, False, "hub", self._th)
+                self.spmm_fn(csr, X, out, rows, False, "hub", self._th, own=own)
                 ev = self._event(("hub", h, c))
                 ev.record(self._hub)
                 done.append(ev)
@@ -847,6 +877,7 @@ class CyclicRowPropagator:
             return X0 if output == "replicated" else X0[torch.as_tensor(self.row_index,
                                                                        device=X0.device)]
         Fp = F
+        src_own = False  # X0 is the caller's tensor (never pad-written / pad-read)
         if X0.is_cuda:
             from . import _lib
             from .propagate import aligned_ld
@@ -861,6 +892,7 @@ class CyclicRowPropagator:
                     _lib.ptr(X0), X0.stride(0), _lib.ptr(Xa), Fp, n, F,
                     _lib.stream_handle(X0.device)), "pad_rows_f32")
                 X0 = Xa
+                src_own = True
         G, R, GR = s.groups, s.rows, s.group_rows
         PGR = s.world_size * GR                   # exchange-buffer rows per group
         self._th = self._thresholds(F)
@@ -878,6 +910,7 @@ class CyclicRowPropagator:
                     raise ValueError(f"out must be [{R}, {F}] (local rows, padding included)")
                 dst = out
             W = min(dst.shape[1], src.shape[1])
+            own = (src_own, exchanged)  # dst = out (a caller's) on the last, unexchanged hop
             passes = [(s.csr_input, None)] if h == 0 else [(s.sub[g], g) for g in range(G)]
             new_works = []
             for pi, (csr, g) in enumerate(passes):
@@ -887,17 +920,18 @@ class CyclicRowPropagator:
                 if pi == len(passes) - 1 and exchanged:
                     chunks = [(c * GR, (c + 1) * GR) for c in range(G)]
                     split = h == 0 and X0.is_cuda and not self.host_staging
-                    hub_done = (self._hub_first(csr, src[:, :W], dst[:, :W], chunks, h) if split
-                                else [None] * G)
+                    hub_done = (self._hub_first(csr, src[:, :W], dst[:, :W], chunks, h, own)
+                                if split else [None] * G)
                     for c, rows in enumerate(chunks):  # final pass in row chunks, each sent at once
                         self.spmm_fn(csr, src[:, :W], dst[:, :W], rows, acc,
-                                     "light" if split else "all", self._th)
+                                     "light" if split else "all", self._th, own=own)
                         new_works.append(self._issue(full[c * PGR:(c + 1) * PGR],
                                                      dst[c * GR:(c + 1) * GR], (h, c), hub_done[c]))
                 else:
-                    self.spmm_fn(csr, src[:, :W], dst[:, :W], (0, R), acc, "all", self._th)
+                    self.spmm_fn(csr, src[:, :W], dst[:, :W], (0, R), acc, "all", self._th,
+                                 own=own)
             if exchanged:
-                works, src = new_works, full
+                works, src, src_own = new_works, full, True
             else:
                 return dst[:s.n_valid]
         for w in works:

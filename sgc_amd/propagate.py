@@ -391,12 +391,15 @@ class SpmmLaunch:
     arguments are built once and each call only passes the stream.  The
     multi-GPU pipeline replays a dozen launches per step, where the checks
     and lookups of spmm() would cost more host time than the launches take on
-    the GPU.  The tensors must stay alive and unchanged in shape/storage."""
+    the GPU.  The tensors must stay alive and unchanged in shape/storage;
+    keep_tensors=False drops the references to X and out (for caches keyed by
+    their data_ptr/shape/stride, which only replay a launch for live tensors
+    at those addresses -- so a cache never pins a caller's tensor)."""
 
     __slots__ = ("_fn", "_args", "_keep")
 
     def __init__(self, csr: DeviceCSR, X: torch.Tensor, out: torch.Tensor, row_begin=0,
-                 row_end=None, flags=0, threshold=None, hub_threshold=None):
+                 row_end=None, flags=0, threshold=None, hub_threshold=None, keep_tensors=True):
         X = _check_features(X, csr)
         if X.device.type != "cuda":
             raise RuntimeError("SpmmLaunch: ROCm tensors only")
@@ -405,7 +408,7 @@ class SpmmLaunch:
         pl = csr.plan(row_begin, row_end, threshold, hub_threshold, F)
         lib = _lib.load()
         self._fn = lib.sgc_spmm_csr_f32_ex
-        self._keep = (csr, X, out, pl)
+        self._keep = (csr, X, out, pl) if keep_tensors else (csr, pl)
         self._args = (_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val),
                       int(row_begin), int(row_end), _lib.ptr(X), X.stride(0), _lib.ptr(out),
                       out.stride(0), F, _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
