@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--shape reddit]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`bench.py --gpus N` (N > 1) without torchrun's environment launches its own N
+ranks (a torch.distributed.run child, started before anything touches the
+GPU) and relays rank 0's line; its exit status is non-zero if any rank fails.
+N = 1 times the public call itself, sgc_precompute(features, adj, K).
+
 Metric (BASELINE.json): propagated edges/s = hops * nnz(S) / t, where t is
 one sgc_precompute (all K hops of S.X, reference utils.py:92-97) over the
 synthetic Reddit-shape graph (232,965 nodes, 11,606,919 undirected edges,
@@ -61,8 +66,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from sgc_amd import graphs  # noqa: E402
-from sgc_amd.propagate import (DeviceCSR, collect_kernel_timing, kernel_timing,  # noqa: E402
-                               propagate)
+from sgc_amd.propagate import DeviceCSR, collect_launch_timing, kernel_timing  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BASELINE_METRIC = ("propagated edges/sec (K-hop SpMM) + precompute wall-time, "
@@ -193,13 +197,14 @@ def load_traffic(shape, lib_sha):
     return d, os.path.relpath(p, ROOT)
 
 
-def roofline(shape, n, nnz, F, hop_ms, light_ms, hub_ms, lib_sha, launch_desc):
+def roofline(shape, n, nnz, F, hop_ms, light_ms, hub_ms, lib_sha, launch_desc, light_kernel):
     gm = gather_model_bytes(n, nnz, F)
     cb = compulsory_bytes(n, nnz, F)
     t = hop_ms * 1e-3
     pmc, src = load_traffic(shape, lib_sha)
     rec = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "kernel": "spmm_csr_kernel (+ spmm_hub_kernel on its side stream, joined)",
+           "kernel": (f"{light_kernel} (+ spmm_hub_kernel beside it, joined)" if hub_ms else
+                      str(light_kernel)),
            "kernel_mean_ms": hop_ms, "launch_unit": launch_desc,
            "light_kernel_mean_ms": light_ms, "hub_kernel_mean_ms": hub_ms,
            "hub_tail_ms": (max(0.0, hub_ms - light_ms) if hub_ms is not None and light_ms
@@ -222,38 +227,23 @@ def roofline(shape, n, nnz, F, hop_ms, light_ms, hub_ms, lib_sha, launch_desc):
     return rec
 
 
-class HopTimer:
-    """hop_hook for propagate(): events around each hop on the launch stream
-    (the interval joins the hub kernel), plus the library's per-kernel events."""
-
-    def __init__(self):
-        self.on = False
-        self.pairs = []
-        self._s = None
-
-    def __call__(self, phase, h):
-        if not self.on:
-            return
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record()
-        if phase == "start":
-            self._s = ev
-        else:
-            self.pairs.append((self._s, ev))
+class LaunchTimer:
+    """The library's own per-launch HIP events (sgc_timing_*) over the timed
+    region: each SpMM launch's light-kernel and hub-kernel durations, each on
+    the stream it runs on, and its span as the launch stream sees it (hub
+    kernel joined) -- the hop time of the roofline."""
 
     def start(self):
-        self.pairs = []
-        collect_kernel_timing()  # drop anything recorded before
+        collect_launch_timing()  # drop anything recorded before
         kernel_timing(True)
-        self.on = True
 
     def stop(self):
-        self.on = False
         kernel_timing(False)
         torch.cuda.synchronize()
-        hops = [s.elapsed_time(e) for s, e in self.pairs]
-        light, hub = collect_kernel_timing()
-        return hops, light, [h for h in hub if h is not None]
+        light, hub, span, kind = collect_launch_timing()
+        names = [k for k in kind if k]
+        top = max(set(names), key=names.count) if names else None
+        return span, light, [h for h in hub if h is not None], top
 
 
 def mean_or_none(v):
@@ -294,10 +284,17 @@ def timed(step, steps, warmup, distributed, dev, on_start=None, on_stop=None):
 
 
 def single_gpu_shape(shape, args, dev, lib_sha, steps, warmup, S=None, X_host=None, K=None):
-    """One BASELINE config on one GPU through the product path (propagate,
-    the engine under sgc_precompute): throughput, per-kernel times, roofline
-    and the first-call (ingest + plan + propagation) time."""
+    """One BASELINE config on one GPU through the public call itself --
+    sgc_precompute(features, adj, K), reference utils.py:92-97, on a torch COO
+    adjacency whose CSR it caches on the first call (as reddit.py's repeated
+    calls would) -- throughput, per-kernel times, roofline and the first-call
+    (ingest + plan + propagation) time."""
+    from sgc_amd import propagate as prop_mod
     from sgc_amd.utils import sgc_precompute
+    if args.threshold is not None:
+        prop_mod.DEFAULT_HEAVY_THRESHOLD = args.threshold
+    if args.hub_threshold is not None:
+        prop_mod.DEFAULT_HUB_THRESHOLD = args.hub_threshold
     spec = graphs.SHAPES[shape]
     K = K or spec["hops"]
     t_gen = time.perf_counter()
@@ -316,18 +313,13 @@ def single_gpu_shape(shape, args, dev, lib_sha, steps, warmup, S=None, X_host=No
     torch.cuda.synchronize()
     _, first_s = sgc_precompute(X0, adj, K)
     ingest_s = adj._sgc_amd_csr[1].ingest_seconds
-    csr = adj._sgc_amd_csr[1]
-    del adj
-    csr.plan(0, n, args.threshold, args.hub_threshold, F)
-    out_buf = torch.empty((n, F), device=dev)
-    hops = HopTimer()
+    launches = LaunchTimer()
 
-    def step():  # the product path of sgc_precompute (sgc_amd.propagate)
-        return propagate(csr, X0, K, out=out_buf, threshold=args.threshold, hop_hook=hops,
-                         hub_threshold=args.hub_threshold)
+    def step():  # the public call, as the reference's drivers make it
+        return sgc_precompute(X0, adj, K)[0]
 
-    elapsed, step_ms, (hop_ms, light, hub) = timed(step, steps, warmup, False, dev,
-                                                   on_start=hops.start, on_stop=hops.stop)
+    elapsed, step_ms, (hop_ms, light, hub, kernel) = timed(
+        step, steps, warmup, False, dev, on_start=launches.start, on_stop=launches.stop)
     hop_mean = float(np.mean(hop_ms))
     rec = {"value": K * nnz * steps / elapsed, "unit": "edges/s",
            "ms_per_step": elapsed * 1e3 / steps,
@@ -339,9 +331,10 @@ def single_gpu_shape(shape, args, dev, lib_sha, steps, warmup, S=None, X_host=No
            "first_call_seconds": round(first_s, 4), "ingest_seconds": round(ingest_s, 4),
            "generate_seconds": round(t_gen, 2),
            "roofline": roofline(shape, n, nnz, F, hop_mean, mean_or_none(light),
-                                mean_or_none(hub), lib_sha, f"one hop over all {n} rows"),
-           "hop_ms_median": float(np.median(hop_ms))}
-    del X0, out_buf, csr
+                                mean_or_none(hub), lib_sha, f"one hop over all {n} rows", kernel),
+           "hop_ms_median": float(np.median(hop_ms)),
+           "timed_call": "sgc_precompute(features, adj, K) (sgc_amd.utils, the drop-in)"}
+    del X0, adj
     torch.cuda.empty_cache()
     return rec, S, X_host
 
@@ -465,6 +458,31 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
     return step, par, unit
 
 
+def self_launch(args):
+    """`bench.py --gpus N` without torchrun's environment: run
+    `python -m torch.distributed.run --nproc-per-node N bench.py <same args>`
+    as a child (stdout passes through: rank 0 prints the JSON line) and
+    return its exit status (non-zero if any rank failed).  Only
+    torch.cuda.device_count() is asked first, which does not initialise the
+    runtime."""
+    import socket
+    import subprocess
+    n_dev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and n_dev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} over RCCL needs {args.gpus} GPUs, {n_dev} visible "
+              f"(--dist-backend gloo rehearses N ranks sharing the GPUs)", file=sys.stderr)
+        return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -507,9 +525,17 @@ def main():
                     help="N>1 features, replicated output: row chunks of the last hop")
     ap.add_argument("--alt-steps", type=int, default=5,
                     help="N>1: steps timed with the other output mode (0 = skip)")
+    ap.add_argument("--public-steps", type=int, default=5,
+                    help="N>1: steps timed through the public sgc_precompute under the process "
+                         "group (replicated X_K, sgc_amd.multigpu; 0 = skip)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="schedule knob for sgc_set_tuning (results never depend on it)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the ranks here, before anything touches
+        # the GPU (no exec after runtime init), relay rank 0's line, and fail
+        # if any rank fails
+        sys.exit(self_launch(args))
     if args.tune:
         from sgc_amd import _lib
         for kv in args.tune:
@@ -519,8 +545,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world == 1 and args.gpus > 1:
-        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     local_dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
@@ -618,6 +644,26 @@ def main():
         alt = {"output": alt_mode, "parallelism": alt_par, "steps": args.alt_steps,
                "ms_per_step": e_alt * 1e3 / args.alt_steps,
                "value": K * nnz * args.alt_steps / e_alt}
+    public = None
+    if args.public_steps > 0:
+        # the reference's own call, unchanged, under this process group:
+        # sgc_precompute(features, adj, K) -> every rank gets all of X_K
+        from sgc_amd import multigpu
+        from sgc_amd.utils import sgc_precompute
+        rows_, cols_, vals_ = S.coo()
+        adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([rows_, cols_])),
+                                      torch.from_numpy(vals_), (n, n)).to(dev)
+        del rows_, cols_, vals_
+        torch.cuda.synchronize()
+        _, first_pub = sgc_precompute(X0, adj, K)  # ingest + partition set-up
+        e_pub, _, _ = timed(lambda: sgc_precompute(X0, adj, K)[0], args.public_steps, 1, True,
+                            dev)
+        public = {"call": "sgc_precompute(features, adj, K) on every rank (sgc_amd.utils -> "
+                          "sgc_amd.multigpu): replicated X_K", "partition": multigpu.partition_name(),
+                  "steps": args.public_steps, "ms_per_step": e_pub * 1e3 / args.public_steps,
+                  "value": K * nnz * args.public_steps / e_pub,
+                  "first_call_seconds": round(first_pub, 4)}
+        del adj
     if rank == 0:
         rec.update({"value": K * nnz * args.steps / elapsed,
                     "ms_per_step": elapsed * 1e3 / args.steps,
@@ -639,6 +685,8 @@ def main():
         rec["precompute_seconds"] = rec["ms_per_step"] / 1e3
         if alt is not None:
             rec["alt_output"] = alt
+        if public is not None:
+            rec["public_call"] = public
         print(json.dumps(rec), flush=True)
     dist.barrier()
     dist.destroy_process_group()

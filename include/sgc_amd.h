@@ -52,9 +52,6 @@ const char *sgc_last_error(void);
  *   "max_vec":      widest per-lane load, 1, 2 or 4 floats (default 4);
  *   "hub_chunk":    features per hub-kernel workgroup, 32 or 64 (default 0 =
  *                   32 when F <= 192 and X rows are 128-B aligned, else 64);
- *   "hub_priority": 1 = hub kernel on a highest-priority stream (default 0);
- *   "hub_first":    1 = hub kernel on the caller's stream, the light/heavy
- *                   kernel on the side stream (default 0: the reverse);
  *   "hub_stream":   1 = hub kernel on a side stream, concurrent with the
  *                   light kernel; 2 = on the caller's stream before the light
  *                   kernel (serial, no cross-stream events); 0 = default: the
@@ -63,11 +60,7 @@ const char *sgc_last_error(void);
  *                   (0 = default, auto; 2 = 32 lanes x 4 floats per row; 4 =
  *                   16 lanes; 1 = one row per wave with the slice_floats /
  *                   max_vec scheme);
- *   "heavy_packed": 1 = heavy rows of the multi-row light kernel packed
- *                   64/LR per wavefront like light rows; 0 = one wavefront
- *                   per 64*VH-float sub-chunk of a heavy row (default);
- *   "hub_loaders":  loader waves per hub workgroup, 15 (default) or 7;
- *   "light_lds":    dynamic LDS bytes reserved per light workgroup (0).
+ *   "hub_loaders":  loader waves per hub workgroup, 15 (default) or 7.
  * sgc_get_tuning returns -1 for an unknown key. */
 int sgc_set_tuning(const char *key, int64_t value);
 int64_t sgc_get_tuning(const char *key);
@@ -211,6 +204,12 @@ int sgc_spmm_csr_f32(const int32_t *row_ptr, const int32_t *col_idx, const float
 int sgc_timing_enable(int on);
 int sgc_timing_collect(float *light_ms_host, float *hub_ms_host, int64_t capacity,
                        int64_t *n_host);
+/* Same, plus per launch: span_ms_host[i] = the whole launch (first kernel
+ * start to the later kernel end: what the caller's stream waits for) and
+ * light_kernel_host[i] = which light/heavy-row kernel ran (0 spmm_csr_kernel,
+ * 1 spmm_rows_kernel, -1 none: a hub-only launch).  Either may be NULL. */
+int sgc_timing_collect_ex(float *light_ms_host, float *hub_ms_host, float *span_ms_host,
+                          int32_t *light_kernel_host, int64_t capacity, int64_t *n_host);
 
 /* Same, with flags.
  * Layout, for buffers whose rows are padded (the engine's own 128-B-row
@@ -336,6 +335,34 @@ int sgc_propagate_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const 
                           int64_t n_rows, const float *X0, int64_t ldx, float *out,
                           int64_t ldo, int64_t F, int32_t K, void *workspace,
                           int64_t workspace_bytes, int32_t n_threads);
+
+/* ---------------------------------------------------------------------------
+ * One process, several GPUs (the multi-GPU form of the one
+ * call reddit.py:43 makes, sgc_precompute -> utils.py:92-97).  The engine
+ * splits the feature columns over the devices: device d pulls its column
+ * block of X_0 from the home device (peer reads over xGMI), runs all K hops
+ * over its own replica of S (no exchange between hops: column f of X_{k+1}
+ * depends on column f of X_k only) and stores its block of X_K straight into
+ * `out` on the home device.  Bit-identical to sgc_propagate_f32.
+ *   sgc_mgpu_init(ndev, devices): devices[0] = home device (where the CSR,
+ *     X_0 and out live); enables peer access between every pair, one stream
+ *     per entry.  An index may repeat (virtual devices sharing one GPU).
+ *     Re-initialising frees the previous engine and its attachments.
+ *   sgc_mgpu_attach: replicate the CSR (home-device pointers, n_rows square)
+ *     to every other device -- synchronous, once per adjacency -- and return
+ *     a handle.  The caller keeps the home arrays alive until detach.
+ *   sgc_mgpu_propagate: X_K = S^K X_0 (K >= 1) into out (row stride ldo),
+ *     asynchronous on `stream` (home device): every device waits for the work
+ *     already on `stream`, and `stream` waits for every device.
+ *   sgc_mgpu_detach / sgc_mgpu_finalize: free one attachment / everything.
+ * Replaces: the torch.spmm loop of utils.py:94-95 spread over the node. */
+int sgc_mgpu_init(int ndev, const int *devices);
+int sgc_mgpu_attach(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                    int64_t n_rows, int64_t nnz, void *stream, int64_t *handle);
+int sgc_mgpu_propagate(int64_t handle, const float *X0, int64_t ldx, float *out, int64_t ldo,
+                       int64_t F, int32_t K, void *stream);
+int sgc_mgpu_detach(int64_t handle);
+int sgc_mgpu_finalize(void);
 
 #ifdef __cplusplus
 }

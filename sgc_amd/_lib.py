@@ -57,6 +57,7 @@ SIGNATURES = {
                                            _p, _i64, _p, _i64, _p]),
     "sgc_timing_enable": (ctypes.c_int, [ctypes.c_int]),
     "sgc_timing_collect": (ctypes.c_int, [_p, _p, _i64, ctypes.POINTER(_i64)]),
+    "sgc_timing_collect_ex": (ctypes.c_int, [_p, _p, _p, _p, _i64, ctypes.POINTER(_i64)]),
     "sgc_coo_to_csr_cpu": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i64, _p, _p, _p,
                                           ctypes.POINTER(_u32)]),
     "sgc_spmm_csr_f32_cpu": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, _i64, _p, _i64, _i64,
@@ -66,6 +67,11 @@ SIGNATURES = {
     "sgc_propagate_cpu_workspace": (_i64, [_i64, _i64, _i32]),
     "sgc_propagate_f32_cpu": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _i32,
                                              _p, _i64, _i32]),
+    "sgc_mgpu_init": (ctypes.c_int, [ctypes.c_int, _p]),
+    "sgc_mgpu_attach": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, ctypes.POINTER(_i64)]),
+    "sgc_mgpu_propagate": (ctypes.c_int, [_i64, _p, _i64, _p, _i64, _i64, _i32, _p]),
+    "sgc_mgpu_detach": (ctypes.c_int, [_i64]),
+    "sgc_mgpu_finalize": (ctypes.c_int, []),
 }
 
 ABI_VERSION = 1

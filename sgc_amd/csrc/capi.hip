@@ -59,6 +59,8 @@ int set_tuning(const char *key, int64_t value);
 int64_t get_tuning(const char *key);
 int timing_enable(int on);
 int timing_collect(float *light_ms, float *hub_ms, int64_t capacity, int64_t *n_host);
+int timing_collect_ex(float *light_ms, float *hub_ms, float *span_ms, int32_t *kernel,
+                      int64_t capacity, int64_t *n_host);
 int coo_to_csr_cpu(const int64_t *rows, const int64_t *cols, const float *vals, int64_t nnz,
                    int64_t n_rows, int64_t n_cols, int32_t *row_ptr, int32_t *col_idx,
                    float *val_out, uint32_t *status_host);
@@ -71,6 +73,13 @@ int propagate_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *v
                   int32_t K, void *workspace, int64_t workspace_bytes, int32_t n_threads);
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                       int64_t ldy, int64_t M, int64_t K, int64_t C, hipStream_t stream);
+int mgpu_init(int ndev, const int *devices);
+int mgpu_finalize();
+int mgpu_attach(const int32_t *row_ptr, const int32_t *col_idx, const float *val, int64_t n,
+                int64_t nnz, hipStream_t stream, int64_t *handle);
+int mgpu_detach(int64_t handle);
+int mgpu_propagate(int64_t handle, const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
+                   int32_t K, hipStream_t stream);
 
 }  // namespace sgc
 
@@ -285,6 +294,12 @@ int sgc_timing_collect(float *light_ms_host, float *hub_ms_host, int64_t capacit
     return timing_collect(light_ms_host, hub_ms_host, capacity, n_host);
 }
 
+int sgc_timing_collect_ex(float *light_ms_host, float *hub_ms_host, float *span_ms_host,
+                          int32_t *light_kernel_host, int64_t capacity, int64_t *n_host) {
+    return timing_collect_ex(light_ms_host, hub_ms_host, span_ms_host, light_kernel_host,
+                             capacity, n_host);
+}
+
 /* ---- host (CPU) twins ---------------------------------------------------- */
 
 int sgc_coo_to_csr_cpu(const int64_t *rows, const int64_t *cols, const float *vals, int64_t nnz,
@@ -324,3 +339,19 @@ int sgc_propagate_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const 
 }
 
 }  // extern "C"
+
+int sgc_mgpu_init(int ndev, const int *devices) { return mgpu_init(ndev, devices); }
+
+int sgc_mgpu_attach(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                    int64_t n_rows, int64_t nnz, void *stream, int64_t *handle) {
+    return mgpu_attach(row_ptr, col_idx, val, n_rows, nnz, as_stream(stream), handle);
+}
+
+int sgc_mgpu_propagate(int64_t handle, const float *X0, int64_t ldx, float *out, int64_t ldo,
+                       int64_t F, int32_t K, void *stream) {
+    return mgpu_propagate(handle, X0, ldx, out, ldo, F, K, as_stream(stream));
+}
+
+int sgc_mgpu_detach(int64_t handle) { return mgpu_detach(handle); }
+
+int sgc_mgpu_finalize(void) { return mgpu_finalize(); }

@@ -37,118 +37,14 @@
 #include <string>
 #include <vector>
 
-#ifndef SGC_NT_STORE
-#define SGC_NT_STORE 0
-#endif
-#ifndef SGC_NT_META
-#define SGC_NT_META 0
-#endif
-
 namespace sgc {
 
 constexpr int kBlock = 256;  // threads per light/heavy workgroup
 
-// Accumulate the C chunks [chunk0, chunk0 + C) of one row and store them.
-template <int V, int C, int U>
-__device__ __forceinline__ void row_chunks(const int *__restrict__ col,
-                                           const float *__restrict__ val, int k0, int k1,
-                                           const float *__restrict__ X, int64_t ldx,
-                                           float *__restrict__ yrow, int F, int chunk0,
-                                           int lane, bool accum) {
-    using VT = typename Vec<V>::T;
-    if (accum && k1 == k0) return;  // nothing to add: the row keeps its partial chains
-    uint32_t boff[C];
-    bool ok[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-        const int f = (chunk0 + c) * (kWave * V) + lane * V;
-        ok[c] = f < F;
-        boff[c] = ok[c] ? uint32_t(f) * 4u : 0u;
-    }
-    VT acc[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-#pragma unroll
-        for (int v = 0; v < V; ++v) set_elem<V>(acc[c], v, 0.0f);
-    if (accum) {  // continue the chains an earlier column-block pass stored
-        const char *Yr = reinterpret_cast<const char *>(yrow);
-#pragma unroll
-        for (int c = 0; c < C; ++c)
-            if (ok[c]) acc[c] = *reinterpret_cast<const VT *>(Yr + boff[c]);
-    }
-
-    const char *Xb = reinterpret_cast<const char *>(X);
-    const int64_t row_bytes = ldx * 4;
-
-    for (int base = k0; base < k1; base += kWave) {
-        const int n = min(kWave, k1 - base);
-        int my_col = 0;
-        float my_val = 0.0f;
-        if (lane < n) {
-#if SGC_NT_META
-            my_col = __builtin_nontemporal_load(col + base + lane);
-            my_val = __builtin_nontemporal_load(val + base + lane);
-#else
-            my_col = col[base + lane];
-            my_val = val[base + lane];
-#endif
-        }
-        // U nonzeros per step; the last step of a batch re-reads its last
-        // valid nonzero for the missing ones (same lines, no extra traffic)
-        // and skips their FMAs with a wave-uniform branch -- padding them
-        // with 0*x would turn a -0.0f accumulator into +0.0f.
-        for (int j = 0; j < n; j += U) {
-            VT xv[U][C];
-            float vv[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int jj = min(j + u, n - 1);
-                const int cj = __builtin_amdgcn_readlane(my_col, jj);
-                vv[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_val), jj));
-                const char *xr = Xb + (int64_t)cj * row_bytes;
-#pragma unroll
-                for (int c = 0; c < C; ++c)
-                    xv[u][c] = *reinterpret_cast<const VT *>(xr + boff[c]);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (j + u < n) {
-#pragma unroll
-                    for (int c = 0; c < C; ++c)
-#pragma unroll
-                        for (int v = 0; v < V; ++v)
-                            set_elem<V>(acc[c], v,
-                                        __builtin_fmaf(vv[u], lane_elem<V>(xv[u][c], v),
-                                                       lane_elem<V>(acc[c], v)));
-                }
-            }
-        }
-    }
-    char *Yb = reinterpret_cast<char *>(yrow);
-#pragma unroll
-    for (int c = 0; c < C; ++c)
-        if (ok[c]) {
-#if SGC_NT_STORE
-            // streamed output: do not let Y rows displace hot X rows in L2
-#pragma unroll
-            for (int v = 0; v < V; ++v)
-                __builtin_nontemporal_store(lane_elem<V>(acc[c], v),
-                                            reinterpret_cast<float *>(Yb + boff[c]) + v);
-#else
-            *reinterpret_cast<VT *>(Yb + boff[c]) = acc[c];
-#endif
-        }
-}
-
-// CSR (col, val) loads: streamed once per slice; SGC_NT_META marks them
-// non-temporal so they need not displace X lines in L2 / the Infinity Cache.
+// CSR (col, val) loads (streamed once per slice).
 template <typename T>
 __device__ __forceinline__ T ld_meta(const T *p) {
-#if SGC_NT_META
-    return __builtin_nontemporal_load(p);
-#else
     return *p;
-#endif
 }
 
 // Software-pipelined form of row_chunks: the X segments of step s+1 (U
@@ -249,21 +145,8 @@ __device__ __forceinline__ void row_chunks_pipe(const int *__restrict__ col,
     char *Yb = reinterpret_cast<char *>(yrow);
 #pragma unroll
     for (int c = 0; c < C; ++c)
-        if (ok[c]) {
-#if SGC_NT_STORE
-#pragma unroll
-            for (int v = 0; v < V; ++v)
-                __builtin_nontemporal_store(lane_elem<V>(acc[c], v),
-                                            reinterpret_cast<float *>(Yb + boff[c]) + v);
-#else
-            *reinterpret_cast<VT *>(Yb + boff[c]) = acc[c];
-#endif
-        }
+        if (ok[c]) *reinterpret_cast<VT *>(Yb + boff[c]) = acc[c];
 }
-
-#ifndef SGC_PIPE
-#define SGC_PIPE 1
-#endif
 
 // Grid: x = work items of one feature slice, y = slice.  Workgroups are
 // dispatched x-fastest, so the chip sweeps the slices one after another and
@@ -295,14 +178,9 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
         if (sub * kWave * VH >= F) return;
         const int row = heavy_rows[h];
         const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
-#if SGC_PIPE
         row_chunks_pipe<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
                                         Y + (int64_t)(row - row_begin) * ldy, F, sub, lane,
                                         accum != 0);
-#else
-        row_chunks<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
-                                   Y + (int64_t)(row - row_begin) * ldy, F, sub, lane, accum != 0);
-#endif
         return;
     }
     const int r = wave - n_heavy_items;
@@ -310,13 +188,8 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int row = row_begin + r;
     const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
     if (k1 - k0 > heavy_threshold) return;  // done as a heavy item or by the hub kernel
-#if SGC_PIPE
     row_chunks_pipe<V, C, U>(col, val, k0, k1, X, ldx, Y + (int64_t)r * ldy, F, slice * C, lane,
                              accum != 0);
-#else
-    row_chunks<V, C, U>(col, val, k0, k1, X, ldx, Y + (int64_t)r * ldy, F, slice * C, lane,
-                        accum != 0);
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -341,19 +214,11 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 //    (same lines, never out of bounds) and skip the FMAs -- still one
 //    sequential FMA chain per element in CSR order.
 // Heavy items (rows above heavy_threshold) come first in the grid, as in
-// spmm_csr_kernel, in one of two forms:
-//  * packed (heavy_packed = 1): R heavy rows per wave, exactly like
-//    light rows (LR lanes and 16-B loads each), taken R at a time from the
-//    plan's list, which is sorted by length, so the rows sharing a wave have
-//    about the same length;
-//  * one wave per 64*VH-float sub-chunk, n_sub per slice (heavy_packed = 0,
-//    the default): 8-B lanes at F % 4 != 0, one row per load instruction,
-//    but twice the loads in flight per row.
-#ifndef SGC_ROWS_U
-#define SGC_ROWS_U 4  // nonzeros per row per step in spmm_rows_kernel (multiple of 4)
-#endif
-constexpr int kRowsU = SGC_ROWS_U;
-static_assert(kRowsU % 4 == 0, "rows kernel reads (col, val) four at a time");
+// spmm_csr_kernel: one wave per 64*VH-float sub-chunk, n_sub per slice (8-B
+// lanes at F % 4 != 0, one row per load instruction, twice the loads in
+// flight per row; packing heavy rows R per wave like light rows measured 1.7x
+// slower on a 76-float slice, profiles/r02/packed_sweep.log).
+constexpr int kRowsU = 4;  // nonzeros per row per step (one b128 (col, val) read each)
 
 template <int LB, int VH, int UH>
 __global__ __launch_bounds__(256) void spmm_rows_kernel(
@@ -361,7 +226,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
     int row_begin, int n_rows, int F, int F_load, int LR, int vec_store, int n_sub,
     const int *__restrict__ heavy_rows, int n_heavy, int heavy_threshold, int accum,
-    int heavy_packed, const int *__restrict__ light_rows) {
+    const int *__restrict__ light_rows) {
     constexpr int V = 4, U = kRowsU < LB / 2 ? kRowsU : LB / 2;
     constexpr int kSteps = LB / U;  // steps per LDS block
     static_assert(kSteps >= 2 && kSteps % 2 == 0, "bad block");
@@ -374,8 +239,8 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kBlock / kWave) + wl));
     const int slice = blockIdx.y;
     const int R = kWave / LR;  // rows per wave (uniform)
-    const int n_heavy_items = heavy_packed ? (n_heavy + R - 1) / R : n_heavy * n_sub;
-    if (!heavy_packed && wave < n_heavy_items) {
+    const int n_heavy_items = n_heavy * n_sub;
+    if (wave < n_heavy_items) {
         const int h = wave / n_sub;
         const int sub = slice * n_sub + (wave - h * n_sub);  // in units of 64*VH floats
         if (sub * kWave * VH >= F) return;
@@ -389,16 +254,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const int sub = lane / LR, l = lane - sub * LR;
     int r = 0, k0 = 0, len = 0;
     bool mine = false;
-    if (wave < n_heavy_items) {  // packed heavy rows: plan entries wave*R + sub
-        const int hi = wave * R + sub;
-        if (sub < R && hi < n_heavy) {
-            const int row = heavy_rows[hi];
-            r = row - row_begin;
-            k0 = row_ptr[row];
-            len = row_ptr[row + 1] - k0;
-            mine = true;
-        }
-    } else if (light_rows) {  // light rows in the plan's order (n_rows of them here)
+    if (light_rows) {  // light rows in the plan's order (n_rows of them here)
         const int w = wave - n_heavy_items;
         if (w * R >= n_rows) return;  // wave-uniform
         const int li = w * R + sub;
@@ -555,37 +411,14 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
 constexpr int kHubInstr = 16;  // consecutive nonzeros per loader lane per round
 constexpr int kHubDepth = 3;   // rounds held in loader registers (17 loads each: vmcnt <= 63)
 constexpr int kHubUnroll = 6;  // lcm(kHubDepth, 2): X ring slot and colv parity compile-time
-#ifndef SGC_HUB_ASM
-#define SGC_HUB_ASM 1  // the chain loop as counted-wait asm (hub_chain_asm)
-#endif
-#ifndef SGC_HUB_PRE
-#define SGC_HUB_PRE (SGC_HUB_ASM ? 4 : 3)
-#endif
-#ifndef SGC_HUB_QUIET_SIMD
-// leave the chain wave's SIMD to it alone (waves w % 4 == 0 idle): measured
-// equal at HC = 32 and 14% slower at HC = 64 (shorter rounds), so the SIMD's
-// other waves are not what holds the chain back (profiles/r02/hub_probe_lib_*.log)
-#define SGC_HUB_QUIET_SIMD 0
-#endif
-#ifndef SGC_HUB_DPP
-#define SGC_HUB_DPP 1  // the asm chain's S values by DPP row broadcast (hub_chain_dpp)
-#endif
-constexpr int kHubPre = SGC_HUB_PRE;  // LDS batches of 4 nonzeros the chain reads ahead
-#ifndef SGC_HUB_SCHED
-#define SGC_HUB_SCHED 0
-#endif
+constexpr int kHubPre = 4;     // LDS batches of 4 nonzeros the chain reads ahead
 
 template <int HC, int NL>
 struct HubShape {
     static constexpr int kSegs = kWave / HC;                     // nonzero runs per loader wave
     static constexpr int kPerLoader = kHubInstr * kSegs;         // nonzeros per loader per round
-    // loader waves that load: all NL, or (SGC_HUB_QUIET_SIMD) all but the
-    // waves sharing the chain wave's SIMD (waves 4, 8, 12 of a 16-wave block)
-    static constexpr int kActive = SGC_HUB_QUIET_SIMD ? NL - NL / 4 : NL;
-    static constexpr int kRound = kActive * kPerLoader;          // nonzeros per round (240 / 480 at NL = 15)
-    // chain read-ahead in batches of 4; HC = 64 fits at most 4 in 160 KB of LDS
-    static constexpr int kPre = (HC == 64 && kHubPre > 4) ? 4 : kHubPre;
-    static constexpr int kPad = 4 * kPre;                        // read-ahead past kRound
+    static constexpr int kRound = NL * kPerLoader;  // nonzeros per round (240 / 480 at NL = 15)
+    static constexpr int kPad = 4 * kHubPre;        // read-ahead past kRound
     // dwords per gxT row: 4 mod 64 (conflict-free b128), and >= kRound + kPad
     // for the FMA loop's read-ahead (kHubPre batches of 4 past the last full batch)
     static constexpr int kStride = (kRound + kPad + 63) / 64 * 64 + 4;
@@ -613,100 +446,6 @@ __device__ unsigned long long g_hub_stamp[5][kStampRounds];
     } while (0)
 #endif
 
-#if SGC_HUB_ASM
-// acc = fmaf(v[k], x[k], acc) for the 4*(4*iters + rem) nonzeros of one
-// round, in order: x at LDS byte address xa (this lane's feature row of the
-// transposed image), v at va (broadcast).  Ring of four slots in v[80:111]
-// (x in v80.., v in v96..), refilled four batches (64 B) ahead; reads past
-// the round stay inside the padded image (kPad >= 16 floats).  Every LDS
-// read is complete (lgkmcnt(0)) before the block ends, so the clobbered
-// registers hold nothing in flight afterwards.  Only LDS reads and VALU.
-__device__ __forceinline__ void hub_chain_asm(float &acc, uint32_t xa, uint32_t va, int iters,
-                                              int rem) {
-    asm volatile(
-        // lgkmcnt also counts scalar loads, which complete out of order:
-        // start with nothing in flight so the counted waits below are exact
-        "s_waitcnt lgkmcnt(0)\n"
-        // prologue: batches 0..3 into slots 0..3
-        "ds_read_b128 v[80:83], %[xa]\n"
-        "ds_read_b128 v[96:99], %[va]\n"
-        "ds_read_b128 v[84:87], %[xa] offset:16\n"
-        "ds_read_b128 v[100:103], %[va] offset:16\n"
-        "ds_read_b128 v[88:91], %[xa] offset:32\n"
-        "ds_read_b128 v[104:107], %[va] offset:32\n"
-        "ds_read_b128 v[92:95], %[xa] offset:48\n"
-        "ds_read_b128 v[108:111], %[va] offset:48\n"
-        "s_cmp_eq_u32 %[it], 0\n"
-        "s_cbranch_scc1 2f\n"
-        "1:\n"
-        "s_waitcnt lgkmcnt(6)\n"
-        "v_fmac_f32 %[acc], v96, v80\n"
-        "v_fmac_f32 %[acc], v97, v81\n"
-        "v_fmac_f32 %[acc], v98, v82\n"
-        "v_fmac_f32 %[acc], v99, v83\n"
-        "ds_read_b128 v[80:83], %[xa] offset:64\n"
-        "ds_read_b128 v[96:99], %[va] offset:64\n"
-        "s_waitcnt lgkmcnt(6)\n"
-        "v_fmac_f32 %[acc], v100, v84\n"
-        "v_fmac_f32 %[acc], v101, v85\n"
-        "v_fmac_f32 %[acc], v102, v86\n"
-        "v_fmac_f32 %[acc], v103, v87\n"
-        "ds_read_b128 v[84:87], %[xa] offset:80\n"
-        "ds_read_b128 v[100:103], %[va] offset:80\n"
-        "s_waitcnt lgkmcnt(6)\n"
-        "v_fmac_f32 %[acc], v104, v88\n"
-        "v_fmac_f32 %[acc], v105, v89\n"
-        "v_fmac_f32 %[acc], v106, v90\n"
-        "v_fmac_f32 %[acc], v107, v91\n"
-        "ds_read_b128 v[88:91], %[xa] offset:96\n"
-        "ds_read_b128 v[104:107], %[va] offset:96\n"
-        "s_waitcnt lgkmcnt(6)\n"
-        "v_fmac_f32 %[acc], v108, v92\n"
-        "v_fmac_f32 %[acc], v109, v93\n"
-        "v_fmac_f32 %[acc], v110, v94\n"
-        "v_fmac_f32 %[acc], v111, v95\n"
-        "ds_read_b128 v[92:95], %[xa] offset:112\n"
-        "ds_read_b128 v[108:111], %[va] offset:112\n"
-        "v_add_u32 %[xa], 64, %[xa]\n"
-        "v_add_u32 %[va], 64, %[va]\n"
-        "s_sub_u32 %[it], %[it], 1\n"
-        "s_cmp_lg_u32 %[it], 0\n"
-        "s_cbranch_scc1 1b\n"
-        "2:\n"
-        // tail: the first `rem` slots hold the last batches of the round
-        "s_cmp_gt_u32 %[rem], 0\n"
-        "s_cbranch_scc0 3f\n"
-        "s_waitcnt lgkmcnt(6)\n"
-        "v_fmac_f32 %[acc], v96, v80\n"
-        "v_fmac_f32 %[acc], v97, v81\n"
-        "v_fmac_f32 %[acc], v98, v82\n"
-        "v_fmac_f32 %[acc], v99, v83\n"
-        "s_cmp_gt_u32 %[rem], 1\n"
-        "s_cbranch_scc0 3f\n"
-        "s_waitcnt lgkmcnt(4)\n"
-        "v_fmac_f32 %[acc], v100, v84\n"
-        "v_fmac_f32 %[acc], v101, v85\n"
-        "v_fmac_f32 %[acc], v102, v86\n"
-        "v_fmac_f32 %[acc], v103, v87\n"
-        "s_cmp_gt_u32 %[rem], 2\n"
-        "s_cbranch_scc0 3f\n"
-        "s_waitcnt lgkmcnt(2)\n"
-        "v_fmac_f32 %[acc], v104, v88\n"
-        "v_fmac_f32 %[acc], v105, v89\n"
-        "v_fmac_f32 %[acc], v106, v90\n"
-        "v_fmac_f32 %[acc], v107, v91\n"
-        "3:\n"
-        "s_waitcnt lgkmcnt(0)\n"
-        : [acc] "+v"(acc), [xa] "+v"(xa), [va] "+v"(va), [it] "+s"(iters)
-        : [rem] "s"(rem)
-        : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91",
-          "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102",
-          "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "scc",
-          "memory");
-}
-#endif
-
-#if SGC_HUB_DPP
 // The chain with the S values off the LDS-read path: one ds_read_b32 per 16
 // nonzeros (lane l reads v[16i + (l & 15)], so each 16-lane row holds the
 // iteration's 16 values) and every FMA takes its S value by a DPP row
@@ -844,7 +583,6 @@ __device__ __forceinline__ void hub_chain_dpp(float &acc, uint32_t xa, uint32_t 
         : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91",
           "v92", "v93", "v94", "v95", "v96", "v97", "scc", "memory");
 }
-#endif
 
 // NL loader waves + the chain wave per workgroup: 15 (1024 threads, ~133 KB
 // of LDS: one workgroup per CU) or 7 (512 threads, ~68 KB: two per CU, half
@@ -858,13 +596,12 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) float gxT[2][HC * Sh::kStride];  // 2 x 66.5 KB
     __shared__ __attribute__((aligned(16)))
-    float gv[2][Sh::kRound + Sh::kPad + (SGC_HUB_DPP ? 32 : 0)];  // + read-ahead
+    float gv[2][Sh::kRound + Sh::kPad + 32];  // + the DPP chain's S read-ahead
     const int lane = threadIdx.x & (kWave - 1);
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
-    // loader index li of wave w (waves sharing SIMD 0 with the chain wave idle
-    // under SGC_HUB_QUIET_SIMD); wave 0 runs the chain
-    const bool loader = w > 0 && (!SGC_HUB_QUIET_SIMD || (w & 3) != 0);
-    const int li = SGC_HUB_QUIET_SIMD ? w - 1 - w / 4 : w - 1;
+    // wave 0 runs the chain, waves 1..NL load (loader index li)
+    const bool loader = w > 0;
+    const int li = w - 1;
     const int h = blockIdx.x / n_chunks;
     const int c = blockIdx.x - h * n_chunks;
     const int row = hub_rows[h];
@@ -928,10 +665,6 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
         g_hub_stamp[4][1] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
-#ifndef SGC_HUB_PRIO
-#define SGC_HUB_PRIO 0  // chain-wave s_setprio level: measured neutral (+-1%), off
-#endif
-    if (SGC_HUB_PRIO && w == 0) __builtin_amdgcn_s_setprio(SGC_HUB_PRIO);
     __syncthreads();
     float acc = 0.0f;
     if (accum && w == 0 && f < F) acc = Y[(int64_t)(row - row_begin) * ldy + f];
@@ -942,128 +675,34 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
             const int r = r0 + s;
             if (r >= n_round) break;  // block-uniform
             const int buf = r & 1;
-#ifndef SGC_HUB_EXPERIMENT
-#define SGC_HUB_EXPERIMENT 0  // timing probes only: 1 = no FMA chain, 2 = no X loads
-#endif
             if (w == 0) HUB_STAMP(0, r);
             if (loader) {
                 if (r + 1 < n_round) store(buf ^ 1, (s + 1) % kHubDepth);
                 if (w == 1) HUB_STAMP(2, r);
                 // ids of round r+D+1 first, so waiting for them (next round)
                 // does not also wait for this round's X loads
-                if (SGC_HUB_EXPERIMENT != 2) {
-                    load_col(r + kHubDepth + 1, (s + kHubDepth + 1) & 1);
-                    load_x(r + kHubDepth, s % kHubDepth, (s + kHubDepth) & 1);
-                }
-            } else if (w == 0 && SGC_HUB_EXPERIMENT != 1) {
+                load_col(r + kHubDepth + 1, (s + kHubDepth + 1) & 1);
+                load_x(r + kHubDepth, s % kHubDepth, (s + kHubDepth) & 1);
+            } else if (w == 0) {
                 const int n = min(Sh::kRound, k1 - (k0 + r * Sh::kRound));
                 const int n4 = n >> 2;
                 // LDS reads run kPre batches of four nonzeros ahead of the FMA
                 // chain (a ds_read's ~64-cycle latency otherwise lands on the
                 // chain every four FMAs); reads past n stay inside the padded
                 // row / value buffers (kStride, gv) and are never used.
-                constexpr int kPre = Sh::kPre;
-#if SGC_HUB_ASM
-                // The chain as one asm loop over four register slots: batch b
-                // (four nonzeros: this lane's X values and their S values,
-                // one ds_read_b128 each) is read four batches before its four
-                // FMAs and waited for with a counted lgkmcnt, so eight LDS
-                // reads stay in flight.  (Left to the compiler, the reads sink
-                // to one batch ahead.)  Same FMA order.  What bounds it is one
-                // wave's LDS read rate: ~35 cycles per 1-KB ds_read_b128 on
-                // gfx950 (scripts/micro/fma_chain.hip: 9-10 cycles per nonzero
-                // alone however deep the ring, vs ~5 for the bare dependent
-                // FMA), ~15 cycles per nonzero beside the loaders' LDS writes
-                // (per-round clock stamps: the chain loop is 95% of each
-                // round; profiles/r02/hub_stamps_*.log).  hub_chain_dpp (the
-                // default) halves the chain's LDS reads -- S by DPP row
-                // broadcast: 9.5 cycles per nonzero alone, and the
-                // 47,857-nonzero row 341 -> 325 us (HC = 64), 306 -> 281 us
-                // (HC = 32), profiles/r02/hub_probe_{base_v2,lib_hubdpp}.log.
-                static_assert(kPre >= 4, "the asm chain reads 4 batches ahead");
+                // The chain as one asm loop (hub_chain_dpp): X values read
+                // four batches of four nonzeros ahead with counted lgkmcnt
+                // waits (left to the compiler the reads sink to one batch
+                // ahead), the round's S values by one ds_read_b32 per 16
+                // nonzeros and a DPP row broadcast per FMA.  Same FMA order.
+                // What bounds it is one wave's LDS read rate: ~35 cycles per
+                // 1-KB ds_read_b128 on gfx950 (scripts/micro/fma_chain.hip:
+                // 9.5 cycles per nonzero alone, ~14-16 beside the loaders' LDS
+                // writes; profiles/r02/micro_fma_chain_v2.log, hub_stamps.log).
                 typedef __attribute__((address_space(3))) const float lds_f;
-                uint32_t xa = (uint32_t)(size_t)(lds_f *)(&gxT[buf][fl * Sh::kStride]);
-                uint32_t va = (uint32_t)(size_t)(lds_f *)(&gv[buf][0]);
-                const int iters = n4 >> 2, rem = n4 & 3;
-#if SGC_HUB_DPP
-                (void)va;
+                const uint32_t xa = (uint32_t)(size_t)(lds_f *)(&gxT[buf][fl * Sh::kStride]);
                 const uint32_t vl = (uint32_t)(size_t)(lds_f *)(&gv[buf][lane & 15]);
-                hub_chain_dpp(acc, xa, vl, iters, rem);
-#else
-                hub_chain_asm(acc, xa, va, iters, rem);
-#endif
-#elif SGC_HUB_SCHED
-                const f4 *xs = reinterpret_cast<const f4 *>(&gxT[buf][fl * Sh::kStride]);
-                const f4 *vs = reinterpret_cast<const f4 *>(&gv[buf][0]);
-                // Ring of 2*kPre slots with compile-time indices: batch b sits
-                // in slot b mod 2kPre, loaded kPre batches before its FMAs, so
-                // no register is copied (a copied load result makes the wave
-                // wait for it) and a sched_barrier keeps each read where it is
-                // issued (left alone, the scheduler sinks it to one batch
-                // before its use and the chain waits on LDS latency).
-                constexpr int kR = 2 * kPre;
-                f4 xr[kR], vr[kR];
-#pragma unroll
-                for (int i = 0; i < kPre; ++i) {
-                    xr[i] = xs[i];
-                    vr[i] = vs[i];
-                }
-                int q = 0;
-                for (; q + kR <= n4; q += kR) {
-#pragma unroll
-                    for (int i = 0; i < kR; ++i) {
-                        const int s = (i + kPre) % kR;
-                        xr[s] = xs[q + i + kPre];
-                        vr[s] = vs[q + i + kPre];
-                        __builtin_amdgcn_sched_barrier(0);
-                        acc = __builtin_fmaf(vr[i][0], xr[i][0], acc);
-                        acc = __builtin_fmaf(vr[i][1], xr[i][1], acc);
-                        acc = __builtin_fmaf(vr[i][2], xr[i][2], acc);
-                        acc = __builtin_fmaf(vr[i][3], xr[i][3], acc);
-                    }
-                }
-                // tail: batches q .. n4-1 (< kR); the first kPre are in slots
-#pragma unroll
-                for (int j = 0; j < kR; ++j)
-                    if (q + j < n4) {
-                        const f4 x = j < kPre ? xr[j] : xs[q + j];
-                        const f4 v = j < kPre ? vr[j] : vs[q + j];
-                        acc = __builtin_fmaf(v[0], x[0], acc);
-                        acc = __builtin_fmaf(v[1], x[1], acc);
-                        acc = __builtin_fmaf(v[2], x[2], acc);
-                        acc = __builtin_fmaf(v[3], x[3], acc);
-                    }
-#else
-                const f4 *xs = reinterpret_cast<const f4 *>(&gxT[buf][fl * Sh::kStride]);
-                const f4 *vs = reinterpret_cast<const f4 *>(&gv[buf][0]);
-                f4 xq[kPre], vq[kPre];
-#pragma unroll
-                for (int i = 0; i < kPre; ++i) {
-                    xq[i] = xs[i];
-                    vq[i] = vs[i];
-                }
-                int q = 0;
-                for (; q + kPre <= n4; q += kPre) {
-#pragma unroll
-                    for (int i = 0; i < kPre; ++i) {
-                        const f4 x = xq[i], v = vq[i];
-                        xq[i] = xs[q + kPre + i];
-                        vq[i] = vs[q + kPre + i];
-                        acc = __builtin_fmaf(v[0], x[0], acc);
-                        acc = __builtin_fmaf(v[1], x[1], acc);
-                        acc = __builtin_fmaf(v[2], x[2], acc);
-                        acc = __builtin_fmaf(v[3], x[3], acc);
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < kPre; ++i)
-                    if (q + i < n4) {
-                        acc = __builtin_fmaf(vq[i][0], xq[i][0], acc);
-                        acc = __builtin_fmaf(vq[i][1], xq[i][1], acc);
-                        acc = __builtin_fmaf(vq[i][2], xq[i][2], acc);
-                        acc = __builtin_fmaf(vq[i][3], xq[i][3], acc);
-                    }
-#endif
+                hub_chain_dpp(acc, xa, vl, n4 >> 2, n4 & 3);
                 const float *xt = &gxT[buf][fl * Sh::kStride];
                 for (int kk = n4 * 4; kk < n; ++kk) acc = __builtin_fmaf(gv[buf][kk], xt[kk], acc);
             }
@@ -1116,31 +755,18 @@ struct SideStream {
     std::mutex mu;
 };
 
-// Hub-kernel stream priority: 1 = the device's highest (meant to let a
-// waiting hub workgroup -- a whole CU's worth of LDS and 16 waves -- be placed
-// before further light-row workgroups), 0 = normal.  Measured neutral (+-1%,
-// profiles/r01_hub_priority_sweep.log), so the default is 0.  Set through
-// sgc_set_tuning("hub_priority").
-static int g_hub_priority = 0;
-
 hipError_t side_stream(SideStream **out) {
     static std::mutex mu;
-    static std::map<std::pair<int, int>, SideStream> per_dev;
+    static std::map<int, SideStream> per_dev;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> lock(mu);
-    SideStream &ss = per_dev[{dev, g_hub_priority}];
+    SideStream &ss = per_dev[dev];
     if (!ss.s) {
-        if (g_hub_priority) {
-            int least = 0, greatest = 0;
-            if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return e;
-            if ((e = hipStreamCreateWithPriority(&ss.s, hipStreamNonBlocking, greatest)) !=
-                hipSuccess)
-                return e;
-        } else if ((e = hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking)) != hipSuccess) {
-            return e;
-        }
+        // (a highest-priority side stream measured neutral, +-1%:
+        // profiles/r01_hub_priority_sweep.log)
+        if ((e = hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking)) != hipSuccess) return e;
         if ((e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming)) != hipSuccess) return e;
         if ((e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming)) != hipSuccess) return e;
     }
@@ -1156,6 +782,8 @@ hipError_t side_stream(SideStream **out) {
 // graph capture.
 struct TimedLaunch {
     hipEvent_t l0 = nullptr, l1 = nullptr, h0 = nullptr, h1 = nullptr;
+    int kernel = -1;      // light kernel: 0 spmm_csr_kernel, 1 spmm_rows_kernel, -1 none
+    bool serial = false;  // hub kernel ran before the light kernel on the same stream
 };
 static std::mutex g_timing_mu;
 static bool g_timing = false;
@@ -1210,29 +838,20 @@ struct TimedGuard {
 
 // Nonzeros per step: light items keep U*C*V <= ~40 registers of gathered X
 // per step; heavy sub-chunk items go deeper (UH).  The pipelined loop holds
-// two steps, so it halves U (measured best at 8 / 16: 48 VGPRs, 8 waves per
-// SIMD, -3% per hop vs. the unpipelined U = 16 / 32; profiles/r01_sweep_pipe.log).
-#ifndef SGC_LIGHT_U_SCALE
-#define SGC_LIGHT_U_SCALE (SGC_PIPE ? 1 : 2)
-#endif
-#ifndef SGC_HEAVY_U
-#define SGC_HEAVY_U (SGC_PIPE ? 16 : 32)
-#endif
-// Dynamic LDS bytes reserved per light/heavy workgroup (unused by the kernel):
-// caps workgroups per CU (160 KB / bytes), i.e. the gathers in flight per CU.
-// 0 = none.  Set through sgc_set_tuning("light_lds").
-static int g_light_lds = 0;
+// two steps (measured best at 8 / 16: 48 VGPRs, 8 waves per SIMD, -3% per hop
+// vs. an unpipelined U = 16 / 32; profiles/r01_sweep_pipe.log).
+constexpr int kHeavyU = 16;
 
 template <int V, int C>
 hipError_t launch_vc(const LaunchArgs &a) {
     constexpr int U0 = (C * V >= 16) ? 2 : (C * V >= 8) ? 4 : 8;
-    constexpr int U = U0 * SGC_LIGHT_U_SCALE > 0 ? U0 * SGC_LIGHT_U_SCALE : 1;
-    constexpr int UH = SGC_HEAVY_U;
+    constexpr int U = U0;
+    constexpr int UH = kHeavyU;
     constexpr int VH = (SGC_HEAVY_VEC < V) ? SGC_HEAVY_VEC : V;
     const int64_t waves = (int64_t)a.n_heavy * (C * V / VH) + a.n_rows;
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     dim3 grid((unsigned)blocks, (unsigned)a.slices);
-    hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH>), grid, dim3(kBlock), g_light_lds, a.stream,
+    hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin, a.n_rows,
                        a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold, a.accum);
     return hipGetLastError();
@@ -1258,13 +877,6 @@ static int g_max_vec = 4;
 // spmm_rows_kernel with 32 / 16 lanes per row on wide launches; 1 = never.
 // profiles/r02/sweep_rows*.  Set through sgc_set_tuning("rows_per_wave").
 static int g_rows_per_wave = 0;
-// Heavy rows in spmm_rows_kernel: 1 = packed R per wave like light rows, 0 =
-// one wave per 64*VH-float sub-chunk (default).  Packed measured equal at
-// F = 602 and 1.7x slower on a single 76-float slice, where the longest heavy
-// rows' latency is the hop's critical path and packing halves each row's
-// loads in flight (profiles/r02/packed_sweep.log).  Set through
-// sgc_set_tuning("heavy_packed").
-static int g_heavy_packed = 0;
 
 template <int LB, int VH>
 hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
@@ -1273,18 +885,17 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     // heavy sub-chunks per slice (unpacked heavy rows): whole 64*VH-float
     // chunks of a slice, or of the launch's width when it is a single slice
     const int n_sub = slices > 1 ? SW / (kWave * VH) : (F_load + kWave * VH - 1) / (kWave * VH);
-    const int64_t heavy_waves = g_heavy_packed ? ((int64_t)a.n_heavy + R - 1) / R
-                                               : (int64_t)a.n_heavy * n_sub;
+    const int64_t heavy_waves = (int64_t)a.n_heavy * n_sub;
     // light items: every row (non-light rows skip themselves), or with a
     // light order exactly the light rows
     const int n_light_items = a.light_rows ? a.n_light : a.n_rows;
     const int64_t waves = heavy_waves + (n_light_items + R - 1) / R;
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     dim3 grid((unsigned)blocks, (unsigned)slices);
-    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, SGC_HEAVY_U>), grid, dim3(kBlock), g_light_lds,
-                       a.stream, a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
+    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU>), grid, dim3(kBlock), 0, a.stream,
+                       a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
                        n_light_items, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
-                       a.heavy_threshold, a.accum, g_heavy_packed, a.light_rows);
+                       a.heavy_threshold, a.accum, a.light_rows);
     return hipGetLastError();
 }
 
@@ -1313,11 +924,6 @@ constexpr int max_chunks(int V) { return 16 / V; }  // <= 16 accumulators per la
 static int g_slice_floats = 128;
 // Hub-kernel feature chunk: 0 = auto (32 on 128-B aligned X rows, else 64).
 static int g_hub_chunk = 0;
-// Which kernel goes first: 0 = hub kernel on the side stream (it starts after
-// the fork-event wait, once the light rows' workgroups hold every CU), 1 = hub
-// kernel on the caller's stream, light/heavy kernel on the side stream (the
-// hub workgroups are placed first).  Set through sgc_set_tuning("hub_first").
-static int g_hub_first = 0;
 // Where the hub kernel runs: 1 = a side stream, concurrent with the light
 // kernel (fork + join events: ~20-30 us of cross-queue synchronisation per
 // launch); 2 = the caller's stream, before the light kernel (serial: costs
@@ -1343,16 +949,6 @@ int set_tuning(const char *key, int64_t value) {
         g_hub_chunk = (int)value;
         return SGC_OK;
     }
-    if (std::string(key) == "hub_priority") {
-        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "hub_priority must be 0 or 1");
-        g_hub_priority = (int)value;
-        return SGC_OK;
-    }
-    if (std::string(key) == "hub_first") {
-        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "hub_first must be 0 or 1");
-        g_hub_first = (int)value;
-        return SGC_OK;
-    }
     if (std::string(key) == "hub_loaders") {
         SGC_REQUIRE(value == 7 || value == 15, SGC_EINVAL, "hub_loaders must be 7 or 15");
         g_hub_loaders = (int)value;
@@ -1369,16 +965,6 @@ int set_tuning(const char *key, int64_t value) {
         g_rows_per_wave = (int)value;
         return SGC_OK;
     }
-    if (std::string(key) == "heavy_packed") {
-        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "heavy_packed must be 0 or 1");
-        g_heavy_packed = (int)value;
-        return SGC_OK;
-    }
-    if (std::string(key) == "light_lds") {
-        SGC_REQUIRE(value >= 0 && value <= 150 * 1024, SGC_EINVAL, "light_lds out of range");
-        g_light_lds = (int)value;
-        return SGC_OK;
-    }
     if (std::string(key) == "max_vec") {
         SGC_REQUIRE(value == 1 || value == 2 || value == 4, SGC_EINVAL, "max_vec must be 1, 2 or 4");
         g_max_vec = (int)value;
@@ -1392,11 +978,7 @@ int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "slice_floats") return g_slice_floats;
     if (key && std::string(key) == "max_vec") return g_max_vec;
     if (key && std::string(key) == "rows_per_wave") return g_rows_per_wave;
-    if (key && std::string(key) == "light_lds") return g_light_lds;
-    if (key && std::string(key) == "heavy_packed") return g_heavy_packed;
     if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
-    if (key && std::string(key) == "hub_priority") return g_hub_priority;
-    if (key && std::string(key) == "hub_first") return g_hub_first;
     if (key && std::string(key) == "hub_stream") return g_hub_stream;
     if (key && std::string(key) == "hub_loaders") return g_hub_loaders;
     return -1;
@@ -1470,13 +1052,13 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
             side_join.side = side;  // from here on every exit joins
             side_join.stream = stream;
-            hs = g_hub_first ? stream : side->s;
-            light_stream = g_hub_first ? side->s : stream;
+            hs = side->s;
         }
         if (timing) {
             SGC_HIP_CHECK(pooled_event(&tl.h0));
             SGC_HIP_CHECK(pooled_event(&tl.h1));
             SGC_HIP_CHECK(hipEventRecord(tl.h0, hs));
+            tl.serial = hs == light_stream;
         }
         const dim3 hub_grid((unsigned)(n_hub * n_chunks));
 #define SGC_LAUNCH_HUB(HCV, NLV)                                                             \
@@ -1553,6 +1135,7 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             SGC_HIP_CHECK(pooled_event(&tl.l0));
             SGC_HIP_CHECK(pooled_event(&tl.l1));
             SGC_HIP_CHECK(hipEventRecord(tl.l0, light_stream));
+            tl.kernel = 1;
         }
         if (LR >= 16)
             e = vh2 ? launch_rows<16, 2>(a, (int)F4, LR, vec_store)
@@ -1577,6 +1160,7 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             SGC_HIP_CHECK(pooled_event(&tl.l0));
             SGC_HIP_CHECK(pooled_event(&tl.l1));
             SGC_HIP_CHECK(hipEventRecord(tl.l0, light_stream));
+            tl.kernel = 0;
         }
         if (V == 4)
             e = dispatch_c<4, max_chunks(4)>(C, a);
@@ -1609,7 +1193,8 @@ int timing_enable(int on) {
     return SGC_OK;
 }
 
-int timing_collect(float *light_ms, float *hub_ms, int64_t capacity, int64_t *n_host) {
+int timing_collect_ex(float *light_ms, float *hub_ms, float *span_ms, int32_t *kernel,
+                      int64_t capacity, int64_t *n_host) {
     SGC_REQUIRE(n_host, SGC_EINVAL, "timing_collect: null n_host");
     std::lock_guard<std::mutex> lock(g_timing_mu);
     const int64_t n = (int64_t)g_timed.size();
@@ -1622,15 +1207,29 @@ int timing_collect(float *light_ms, float *hub_ms, int64_t capacity, int64_t *n_
         SGC_HIP_CHECK(hipEventSynchronize(t.l1));
         SGC_HIP_CHECK(hipEventElapsedTime(&light_ms[i], t.l0, t.l1));
         hub_ms[i] = -1.0f;
+        float span = light_ms[i];
         if (t.h0) {
             SGC_HIP_CHECK(hipEventSynchronize(t.h1));
             SGC_HIP_CHECK(hipEventElapsedTime(&hub_ms[i], t.h0, t.h1));
+            float to_end = 0.0f;
+            if (t.serial) {  // h0 ... h1 l0 ... l1 on one stream
+                SGC_HIP_CHECK(hipEventElapsedTime(&span, t.h0, t.l1));
+            } else {  // the side stream starts at the fork, just before l0
+                SGC_HIP_CHECK(hipEventElapsedTime(&to_end, t.l0, t.h1));
+                span = std::max(span, to_end);
+            }
         }
+        if (span_ms) span_ms[i] = span;
+        if (kernel) kernel[i] = t.kernel;
         for (hipEvent_t ev : {t.l0, t.l1, t.h0, t.h1})
             if (ev) g_event_pool.push_back(ev);
     }
     g_timed.clear();
     return SGC_OK;
+}
+
+int timing_collect(float *light_ms, float *hub_ms, int64_t capacity, int64_t *n_host) {
+    return timing_collect_ex(light_ms, hub_ms, nullptr, nullptr, capacity, n_host);
 }
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,263 @@
+"""sgc_precompute across GPUs behind the reference's own call.
+
+The reference's drivers call `sgc_precompute(features, adj, degree)`
+(reddit.py:43, citation.py:32 -> utils.py:92-97) and expect the whole X_K
+back.  This module lets that unchanged call use every GPU of the node, in
+either of two ways:
+
+* one process per GPU (`torchrun --nproc-per-node N reddit.py`): importing
+  the drop-in binds each process to cuda:LOCAL_RANK, so the caller's
+  `.cuda()` tensors land on its own GPU; on the first sgc_precompute a process
+  group is initialised from torchrun's environment (RCCL over xGMI when every
+  local rank has a GPU of its own, gloo when ranks share one -- the host-staged
+  rehearsal), or the caller's own initialised default group is used.  The K
+  hops then run partitioned (sgc_amd.distributed) and every rank gets the
+  full X_K, as the reference returns it;
+* one process, several devices (`SGC_AMD_DEVICES=all` or `=0,1,2,3`): the
+  native multi-device engine of the C ABI (sgc_mgpu_*, csrc/mgpu.hip) drives
+  all of them from the single call; see `DeviceSet`.
+
+Partition (SGC_AMD_PARTITION): "features" (default) -- each rank runs all K
+hops over the whole S on its block of feature columns, so the only exchange
+is one all-gather of X_K, the least any replicated output can move; "rows"
+(nnz-balanced row blocks, an all-gather of X_k per hop: the north star's 1-D
+row slicing) or "cyclic" (row tiles round-robin, column-ordered exchange).
+Every partition keeps each output element's FMA chain whole and in CSR
+order, so X_K is bit-identical to one GPU's and to the reference.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+PARTITIONS = ("features", "rows", "cyclic")
+
+
+def torchrun_env():
+    """(rank, world, local_rank, local_world) when launched by torchrun with
+    more than one process, else None."""
+    try:
+        world = int(os.environ["WORLD_SIZE"])
+        rank = int(os.environ["RANK"])
+    except (KeyError, ValueError):
+        return None
+    if world <= 1:
+        return None
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    return rank, world, local, local_world
+
+
+def bind_local_device():
+    """Under torchrun, make `cuda` mean cuda:(LOCAL_RANK mod visible GPUs) for
+    this process, so an unchanged driver's `.cuda()` calls land on its own
+    GPU.  No-op without torchrun, without a GPU, or with
+    SGC_AMD_BIND_DEVICE=0.  Returns the device index bound (or None)."""
+    env = torchrun_env()
+    if env is None or os.environ.get("SGC_AMD_BIND_DEVICE", "1") == "0":
+        return None
+    n = torch.cuda.device_count()  # does not initialise the runtime
+    if n == 0:
+        return None
+    d = env[2] % n
+    torch.cuda.set_device(d)
+    return d
+
+
+def process_group(device):
+    """The group sgc_precompute partitions over, or None (one device).
+
+    An initialised default group with world > 1 is used as is.  Under
+    torchrun without one, it is initialised here (env://): backend
+    SGC_AMD_DIST_BACKEND, else "nccl" (RCCL) when every local rank has a GPU of
+    its own and the tensors are on the GPU, else "gloo".
+    SGC_AMD_AUTO_DIST=0 turns the whole multi-process mode off."""
+    if os.environ.get("SGC_AMD_AUTO_DIST", "1") == "0" or not dist.is_available():
+        return None
+    if dist.is_initialized():
+        return dist.group.WORLD if dist.get_world_size() > 1 else None
+    env = torchrun_env()
+    if env is None:
+        return None
+    backend = os.environ.get("SGC_AMD_DIST_BACKEND")
+    if not backend:
+        own_gpu = device.type == "cuda" and torch.cuda.device_count() >= env[3]
+        backend = "nccl" if own_gpu else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=device)
+    else:
+        dist.init_process_group(backend)
+    return dist.group.WORLD
+
+
+def partition_name():
+    p = os.environ.get("SGC_AMD_PARTITION", "features")
+    if p not in PARTITIONS:
+        raise ValueError(f"SGC_AMD_PARTITION must be one of {PARTITIONS}, not {p!r}")
+    return p
+
+
+def _host_csr(csr):
+    """Host copies (numpy) of a DeviceCSR's arrays, cached on it: the row and
+    cyclic partitions slice S on the host once per adjacency."""
+    key = ("host_arrays",)
+    if key not in csr._plans:
+        csr._plans[key] = tuple(t.cpu().numpy() for t in (csr.row_ptr, csr.col_idx, csr.val))
+    return csr._plans[key]
+
+
+def _propagator(csr, group, partition, staging):
+    """The partitioned propagator for (adjacency, group, partition), built once
+    and cached on the adjacency's CSR with its buffers and prepared launches."""
+    from .distributed import (CyclicRowPropagator, FeaturePartitionedPropagator,
+                              RowPartitionedPropagator, make_shard)
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    key = ("dist", id(group), rank, world, partition, staging)
+    prop = csr._plans.get(key)
+    if prop is not None:
+        return prop
+    if partition == "features":
+        prop = FeaturePartitionedPropagator(csr, rank=rank, world_size=world, group=group,
+                                            host_staging=staging)
+    elif partition == "rows":
+        rp, ci, va = _host_csr(csr)
+        shard = make_shard(rp, ci, va, rank, world, csr.device)
+        prop = RowPartitionedPropagator(shard, group=group, host_staging=staging)
+    else:
+        rp, ci, va = _host_csr(csr)
+        groups = 1 if world <= 2 else 2 if world <= 4 else 3
+        prop = CyclicRowPropagator(rp, ci, va, rank, world, csr.device, group=group,
+                                   groups=groups, host_staging=staging)
+    csr._plans[key] = prop
+    return prop
+
+
+def precompute_group(csr, X, K, group):
+    """X_K = S^K X on every rank of `group`, partitioned (the caller has
+    checked shapes and devices).  Collective: every rank must call it with
+    the same adjacency and feature shape."""
+    staging = X.is_cuda and dist.get_backend(group) != "nccl"
+    prop = _propagator(csr, group, partition_name(), staging)
+    return prop.propagate(X, K, output="replicated")
+
+
+# ---------------------------------------------------------------------------
+# One process, several devices: the native engine (sgc_mgpu_*).
+
+def devices_from_env(home):
+    """Devices named by SGC_AMD_DEVICES ("all", or a comma list of indices;
+    the list may repeat an index: virtual devices sharing a GPU, used to
+    rehearse the engine on one GPU), with the caller's device `home` first.
+    None when unset or naming a single device."""
+    spec = os.environ.get("SGC_AMD_DEVICES", "").strip()
+    if not spec:
+        return None
+    if spec == "all":
+        devs = list(range(torch.cuda.device_count()))
+    else:
+        devs = [int(x) for x in spec.split(",") if x.strip()]
+    if home in devs:
+        devs.remove(home)
+    devs = [home] + devs
+    return devs if len(devs) > 1 else None
+
+
+class DeviceSet:
+    """The native multi-device engine for one ordered device list
+    (csrc/mgpu.hip): sgc_mgpu_init once per process, one attached replica set
+    per adjacency (cached on its DeviceCSR, detached when that is freed)."""
+
+    _current = None
+    _generation = 0
+
+    def __init__(self, devices):
+        from . import _lib
+        import ctypes
+        self.devices = list(devices)
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        _lib.check(_lib.load().sgc_mgpu_init(len(self.devices), ctypes.cast(arr, ctypes.c_void_p)),
+                   "mgpu_init")
+        DeviceSet._generation += 1
+        self.generation = DeviceSet._generation  # handles of an earlier engine are void
+
+    @classmethod
+    def get(cls, devices):
+        cur = cls._current
+        if cur is None or cur.devices != list(devices):
+            if cur is not None:
+                cur.finalize()
+            cls._current = cur = cls(devices)
+        return cur
+
+    def finalize(self):
+        from . import _lib
+        _lib.check(_lib.load().sgc_mgpu_finalize(), "mgpu_finalize")
+        if DeviceSet._current is self:
+            DeviceSet._current = None
+
+    def attach(self, csr):
+        """Handle of csr's replicas on every device (made once: one copy of S
+        per device, plus its launch plans)."""
+        import weakref
+        from . import _lib
+        key = ("mgpu", self.generation)
+        h = csr._plans.get(key)
+        if h is None:
+            lib = _lib.load()
+            out = _lib._i64(0)
+            with torch.cuda.device(csr.device):
+                _lib.check(lib.sgc_mgpu_attach(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
+                                               _lib.ptr(csr.val), csr.n_rows, csr.nnz,
+                                               _lib.stream_handle(csr.device),
+                                               _ctypes_byref(out)), "mgpu_attach")
+            h = int(out.value)
+            csr._plans[key] = h
+            weakref.finalize(csr, _detach, h)
+        return h
+
+    def propagate(self, csr, X, K, out):
+        from . import _lib
+        h = self.attach(csr)
+        with torch.cuda.device(X.device):
+            _lib.check(_lib.load().sgc_mgpu_propagate(h, _lib.ptr(X), X.stride(0), _lib.ptr(out),
+                                                      out.stride(0), X.shape[1], int(K),
+                                                      _lib.stream_handle(X.device)),
+                       "mgpu_propagate")
+        return out
+
+
+def _ctypes_byref(x):
+    import ctypes
+    return ctypes.byref(x)
+
+
+def _detach(handle):
+    try:
+        from . import _lib
+        _lib.load().sgc_mgpu_detach(handle)
+    except Exception:  # interpreter shutdown: the engine is gone with the process
+        pass
+
+
+def precompute_devices(csr, X, K, devices):
+    """X_K on the caller's device, computed by the devices in `devices`
+    (devices[0] = X's device) through the native engine."""
+    n, F = X.shape
+    out = torch.empty((n, F), dtype=torch.float32, device=X.device)
+    if n == 0 or F == 0:
+        return out
+    return DeviceSet.get(devices).propagate(csr, X, K, out)
+
+
+def feature_blocks(F, parts, align=4):
+    """Column blocks of the feature partition (the same rule as
+    sgc_amd.distributed.feature_bounds, which the native engine mirrors)."""
+    from .distributed import feature_bounds
+    b, _ = feature_bounds(F, parts, align)
+    return [(int(b[i]), int(b[i + 1])) for i in range(parts)]
+
+
+__all__ = ["torchrun_env", "bind_local_device", "process_group", "precompute_group",
+           "devices_from_env", "DeviceSet", "precompute_devices", "feature_blocks",
+           "PARTITIONS"]

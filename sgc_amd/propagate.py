@@ -348,6 +348,15 @@ def _check_features(X, csr):
     return X
 
 
+def check_propagation_inputs(csr: DeviceCSR, X: torch.Tensor):
+    """The checks propagate() makes (types, devices, shapes, a square S);
+    returns X with unit column stride."""
+    X = _check_features(X, csr)
+    if csr.n_rows != csr.n_cols:
+        raise RuntimeError("sgc_amd: propagation needs a square adjacency")
+    return X
+
+
 def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
          use_plan=True, threshold=None, hub_threshold=None, flags=0):
     """One hop Y = S[row_begin:row_end] . X (bit-exact with torch.spmm on CPU).
@@ -451,9 +460,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
     last hop writes the contiguous [N, F] result.  hop_hook(phase, h) is called
     around each hop's launch ("start"/"end", for event timing).
     native_loop=True runs the same loop inside the C ABI call instead."""
-    X = _check_features(X, csr)
-    if csr.n_rows != csr.n_cols:
-        raise RuntimeError("sgc_amd: propagation needs a square adjacency")
+    X = check_propagation_inputs(csr, X)
     n, F = X.shape
     if out is None:
         out = torch.empty((n, F), dtype=torch.float32, device=X.device)
@@ -577,6 +584,30 @@ def collect_kernel_timing(capacity=1 << 16):
     k = int(n.value)
     return [float(light[i]) for i in range(k)], [float(hub[i]) if hub[i] >= 0 else None
                                                  for i in range(k)]
+
+
+def collect_launch_timing(capacity=1 << 16):
+    """Per SpMM launch since the last collect: (light_ms, hub_ms, span_ms,
+    light_kernel) lists -- span = the whole launch as the caller's stream
+    sees it (hub kernel joined); light_kernel = "spmm_csr_kernel",
+    "spmm_rows_kernel" or None (a hub-only launch); hub_ms None without hub
+    rows."""
+    import ctypes
+    lib = _lib.load()
+    light = (ctypes.c_float * capacity)()
+    hub = (ctypes.c_float * capacity)()
+    span = (ctypes.c_float * capacity)()
+    kind = (ctypes.c_int32 * capacity)()
+    n = _lib._i64(0)
+    _lib.check(lib.sgc_timing_collect_ex(*(ctypes.cast(b, ctypes.c_void_p)
+                                           for b in (light, hub, span, kind)),
+                                         capacity, ctypes_byref(n)), "timing_collect_ex")
+    names = {0: "spmm_csr_kernel", 1: "spmm_rows_kernel"}
+    k = int(n.value)
+    return ([float(light[i]) for i in range(k)],
+            [float(hub[i]) if hub[i] >= 0 else None for i in range(k)],
+            [float(span[i]) for i in range(k)],
+            [names.get(int(kind[i])) for i in range(k)])
 
 
 def linear(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, out=None):

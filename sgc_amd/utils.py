@@ -19,8 +19,13 @@ import numpy as np
 import scipy.sparse as sp
 import torch
 
+from . import multigpu
 from .normalization import aug_normalize_on_device, fetch_normalization, row_normalize
-from .propagate import csr_of, propagate, to_torch_coo
+from .propagate import check_propagation_inputs, csr_of, propagate, to_torch_coo
+
+# under torchrun: this process's `.cuda()` is its own GPU (cuda:LOCAL_RANK),
+# so an unchanged reddit.py / citation.py spreads over the node's GPUs
+multigpu.bind_local_device()
 
 
 def parse_index_file(filename):
@@ -80,7 +85,11 @@ def sgc_precompute(features, adj, degree):
     twin (the reference's --no-cuda mode); mixed devices raise RuntimeError.
     degree <= 0 returns the input tensor object itself (the reference's loop
     body never runs).  The result is bit-identical to the reference's
-    torch.spmm chain on CPU for the same inputs, on either device."""
+    torch.spmm chain on CPU for the same inputs, on either device -- and on
+    any number of GPUs: under torchrun (or an initialised process group of
+    world > 1) the hops run partitioned over the ranks and every rank gets
+    the whole X_K; with SGC_AMD_DEVICES one process drives several GPUs
+    (sgc_amd.multigpu)."""
     if degree <= 0:
         t = perf_counter()
         return features, perf_counter() - t
@@ -89,10 +98,24 @@ def sgc_precompute(features, adj, degree):
         torch.cuda.synchronize(dev)
     t = perf_counter()
     csr = csr_of(adj)
-    out = propagate(csr, features, degree)
+    out = _propagate_on_node(csr, features, degree)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     return out, perf_counter() - t
+
+
+def _propagate_on_node(csr, X, K):
+    """One GPU, the process group's GPUs, or this process's device set."""
+    group = multigpu.process_group(X.device)
+    if group is not None:
+        X = check_propagation_inputs(csr, X)
+        return multigpu.precompute_group(csr, X, K, group)
+    if X.device.type == "cuda":
+        devices = multigpu.devices_from_env(X.device.index)
+        if devices:
+            X = check_propagation_inputs(csr, X)
+            return multigpu.precompute_devices(csr, X, K, devices)
+    return propagate(csr, X, K)
 
 
 def set_seed(seed, cuda):

@@ -23,7 +23,7 @@ def test_byte_models_reddit():
 
 def test_roofline_refuses_traffic_of_another_build():
     rec = bench.roofline("reddit", REDDIT["n"], REDDIT["nnz"], REDDIT["F"], 4.65, 4.45, 4.6,
-                         "0" * 64, "one hop")
+                         "0" * 64, "one hop", "spmm_rows_kernel")
     assert rec["traffic"] is None and "refused" in rec["traffic_source"]
     assert rec["frac"] == pytest.approx(rec["compulsory_frac"])
     assert rec["hub_tail_ms"] == pytest.approx(0.15)
@@ -38,7 +38,7 @@ def test_roofline_uses_matching_pmc_record(shape):
     assert traffic is not None and traffic["hbm_bytes_per_launch"] > 0
     ms = float(pmc["kernel_ms"])  # the hop time the counters were taken over
     rec = bench.roofline(shape, REDDIT["n"], REDDIT["nnz"], REDDIT["F"], ms, ms, None,
-                         pmc_sha, "one hop")
+                         pmc_sha, "one hop", "spmm_rows_kernel")
     t = ms * 1e-3
     assert rec["traffic"] == traffic["hbm_bytes_per_launch"]
     assert rec["frac"] == pytest.approx(rec["traffic"] / t / 1e9 / bench.HBM_PEAK_GBS)
@@ -48,3 +48,13 @@ def test_roofline_uses_matching_pmc_record(shape):
 def test_host_cores_positive():
     n, how = bench.host_cores()
     assert n >= 1 and "sched_getaffinity" in how
+
+
+def test_self_launch_refuses_more_ranks_than_gpus(monkeypatch, capsys):
+    """--gpus N over RCCL with fewer visible GPUs: refused before any rank is
+    started (exit status 2), without touching the GPU runtime."""
+    import argparse
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 1)
+    args = argparse.Namespace(gpus=4, dist_backend="nccl")
+    assert bench.self_launch(args) == 2
+    assert "needs 4 GPUs" in capsys.readouterr().err

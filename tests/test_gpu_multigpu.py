@@ -1,0 +1,204 @@
+"""The multi-GPU paths on the one GPU a test box has, bit-exact.
+
+* the native multi-device engine (sgc_mgpu_*, csrc/mgpu.hip) with VIRTUAL
+  devices -- the same index repeated: every entry its own stream, buffers and
+  column block, exactly the code an 8-GPU node runs minus the xGMI hops;
+* the unchanged `sgc_precompute` under torchrun (2 ranks sharing the GPU over
+  gloo: the group is initialised by the drop-in from torchrun's environment),
+  and the reddit driver run that way end to end;
+* `bench.py --gpus 2` launching its own ranks (what the driver's scaling run
+  does when it does not use torchrun itself);
+* the P = 8 partitions at FULL BASELINE size (8 gloo ranks on the GPU, the
+  product propagators, X_K assembled from every rank's rows) against the
+  reference's own hashes: Reddit K = 2 for the row, cyclic, feature and 2-D
+  tile partitions, RMAT K = 3 for the row partition.
+"""
+import hashlib
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _torchrun(nproc, script_args, env_extra=None, timeout=600):
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.update(env_extra or {})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", *script_args]
+    return subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True,
+                          timeout=timeout)
+
+
+def _last_json(text):
+    for line in reversed(text.strip().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise AssertionError(f"no JSON line in output:\n{text[-2000:]}")
+
+
+def _csr(case, oracle):
+    from sgc_amd.propagate import DeviceCSR
+    n = int(case["n"])
+    rp, ci, va = oracle.coo_to_csr(n, n, case["rows"], case["cols"], case["vals"])
+    return DeviceCSR.from_host_arrays(rp, ci, va, device="cuda")
+
+
+# ---------------------------------------------------------------------------
+# native multi-device engine, virtual devices
+
+@pytest.mark.parametrize("ndev", [2, 3, 8])
+@pytest.mark.parametrize("name,K", [("norm_n48_F602", 2), ("hub1000_F130", 2),
+                                    ("norm_n48_F65", 3), ("isolated_F17", 1),
+                                    ("raw_unsorted_dups_F7", 3), ("special_values_F11", 2),
+                                    ("no_edges_F5", 2), ("norm_n48_F3", 3)])
+def test_mgpu_engine_virtual_devices_bit_exact(tiny_cases, oracle, ndev, name, K):
+    """Feature blocks over ndev virtual devices (some empty when F < 4 ndev),
+    pulled from the home device, K local hops, the last one stored into the
+    caller's X_K: equal to the reference's X_K bit for bit, twice (buffers
+    and plans reused)."""
+    from sgc_amd.multigpu import DeviceSet
+    case = tiny_cases[name]
+    csr = _csr(case, oracle)
+    X = torch.from_numpy(case["X"]).cuda()
+    ds = DeviceSet.get([0] * ndev)
+    want = case[f"Y{K}"]
+    for _ in range(2):
+        out = torch.full(X.shape, float("nan"), device="cuda")
+        ds.propagate(csr, X, K, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+def test_mgpu_engine_strided_input_and_output(tiny_cases, oracle):
+    """X_0 a column view of a wider tensor, X_K written into a column view:
+    no byte outside the view changes (the last hop never pad-writes Y)."""
+    from sgc_amd.multigpu import DeviceSet
+    case = tiny_cases["norm_n48_F130"]
+    csr = _csr(case, oracle)
+    n, F = case["X"].shape
+    big = torch.randn(n, F + 7, device="cuda")
+    big[:, 3:3 + F] = torch.from_numpy(case["X"]).cuda()
+    dst = torch.full((n, F + 9), 7.0, device="cuda")
+    DeviceSet.get([0, 0, 0, 0]).propagate(csr, big[:, 3:3 + F], 2, dst[:, 5:5 + F])
+    torch.cuda.synchronize()
+    got = dst.cpu().numpy()
+    assert np.array_equal(got[:, 5:5 + F].view(np.uint32), case["Y2"].view(np.uint32))
+    assert (got[:, :5] == 7.0).all() and (got[:, 5 + F:] == 7.0).all()
+
+
+def test_sgc_precompute_with_device_set_env(tiny_cases, oracle, monkeypatch):
+    """SGC_AMD_DEVICES routes the unchanged call through the engine."""
+    from sgc_amd.utils import sgc_precompute
+    case = tiny_cases["norm_n48_F602"]
+    n = int(case["n"])
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([case["rows"], case["cols"]])),
+                                  torch.from_numpy(case["vals"]), (n, n)).cuda()
+    monkeypatch.setenv("SGC_AMD_DEVICES", "0,0,0,0")
+    out, secs = sgc_precompute(torch.from_numpy(case["X"]).cuda(), adj, 2)
+    assert secs > 0
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), case["Y2"].view(np.uint32))
+    assert any(k[0] == "mgpu" for k in adj._sgc_amd_csr[1]._plans if isinstance(k, tuple))
+
+
+@pytest.mark.slow
+def test_mgpu_engine_reddit_shape_hash(shapes_golden):
+    """Eight virtual devices at full Reddit shape (76-column blocks): the
+    reference's X_2 hash."""
+    from sgc_amd import graphs
+    from sgc_amd.multigpu import DeviceSet
+    from sgc_amd.propagate import DeviceCSR
+    g = shapes_golden["reddit"]
+    S = graphs.synthetic_graph("reddit", seed=g["seed"])
+    X = torch.from_numpy(graphs.synthetic_features("reddit", g["n"], g["features"],
+                                                   seed=g["feature_seed"])).cuda()
+    csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device="cuda")
+    out = torch.empty_like(X)
+    DeviceSet.get([0] * 8).propagate(csr, X, 2, out)
+    torch.cuda.synchronize()
+    assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == g["outputs"]["2"]["sha"]
+
+
+# ---------------------------------------------------------------------------
+# sgc_precompute under torchrun, the reddit driver, bench.py self-launch
+
+@pytest.mark.parametrize("partition", ["features", "rows", "cyclic"])
+def test_sgc_precompute_under_torchrun_matches_one_gpu(tmp_path, partition):
+    """Two torchrun ranks sharing the GPU (gloo, chosen by the drop-in because
+    there are fewer GPUs than ranks) run the unchanged sgc_precompute on the
+    reddit driver's synthetic graph: both get the X_K one GPU computes."""
+    from drivers.reddit import synthetic_reddit
+    from sgc_amd.utils import sgc_precompute
+    r = _torchrun(2, ["tests/rank_precompute.py", str(tmp_path), "20000"],
+                  {"SGC_AMD_PARTITION": partition}, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(2)]
+    adj, _, features, _, _, _, _ = synthetic_reddit(20000)
+    one, _ = sgc_precompute(features, adj, 2)
+    want = hashlib.sha256(one.cpu().numpy().tobytes()).hexdigest()
+    for rec in recs:
+        assert rec["world"] == 2 and rec["backend"] == "gloo" and rec["repeat_equal"]
+        assert rec["sha"] == want
+
+
+def test_reddit_driver_runs_under_torchrun():
+    """drivers/reddit.py (the reference's reddit.py flow) unchanged under
+    torchrun: every rank precomputes through the partitioned path and trains."""
+    r = _torchrun(2, ["drivers/reddit.py", "--synthetic", "20000"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count("Total Time:") == 2
+
+
+def test_bench_self_launch_two_ranks():
+    """`bench.py --gpus 2` without torchrun's environment starts its own two
+    ranks (gloo: they share this GPU) and prints rank 0's line."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--shape",
+           "pubmed", "--steps", "2", "--warmup", "1", "--alt-steps", "1", "--public-steps", "1"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _last_json(r.stdout)
+    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["steps"] == 2
+    assert rec["public_call"]["value"] > 0 and "auto-selected" in rec["config"]["parallelism"]
+
+
+# ---------------------------------------------------------------------------
+# P = 8 at full size (gloo, 8 ranks on this GPU)
+
+@pytest.fixture(scope="module")
+def dist_cache(tmp_path_factory):
+    return str(tmp_path_factory.mktemp("dist_check"))
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("shape,partition,extra", [
+    ("reddit", "rows", []),
+    ("reddit", "rows", ["--row-chunks", "4"]),
+    ("reddit", "cyclic", ["--groups", "3"]),
+    ("reddit", "features", []),
+    ("reddit", "tiles", ["--col-blocks", "2"]),
+    ("rmat", "rows", [])])
+def test_p8_partition_full_size_bit_exact(dist_cache, shape, partition, extra):
+    r = _torchrun(8, ["scripts/dist_check.py", "--shape", shape, "--partition", partition,
+                      "--cache", dist_cache, *extra], timeout=840)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _last_json(r.stdout)
+    assert rec["world"] == 8 and rec["bit_exact_vs_reference_hash"], rec

@@ -1,0 +1,108 @@
+"""sgc_precompute across processes behind the reference's own call
+(sgc_amd.multigpu; reference reddit.py:43 -> utils.py:92-97), on CPU over gloo.
+
+Each worker is started the way torchrun starts a rank -- RANK / WORLD_SIZE /
+LOCAL_RANK / MASTER_* in its environment, no process group yet -- and calls
+the unchanged `sgc_precompute(features, adj, K)`: the first call initialises
+the group from that environment and the hops run partitioned.  Every rank's
+X_K must equal the reference's (the golden vectors) bit for bit, for each
+partition.  The GPU versions (RCCL, the one-GPU gloo rehearsal, the native
+multi-device engine) are in tests/test_gpu_multigpu.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _torchrun_like_worker(rank, world, port, case, K, partition, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), SGC_AMD_PARTITION=partition)
+    import torch.distributed as dist
+    from sgc_amd.utils import sgc_precompute
+    try:
+        n = int(case["n"])
+        adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([case["rows"], case["cols"]])),
+                                      torch.from_numpy(case["vals"]), (n, n))
+        X = torch.from_numpy(case["X"])
+        out, secs = sgc_precompute(X, adj, K)
+        again, _ = sgc_precompute(X, adj, K)  # cached partition, buffers reused
+        q.put((rank, out.numpy().copy(), bool(torch.equal(out, again)), dist.get_world_size(),
+               secs >= 0))
+    finally:
+        import torch.distributed as dist2
+        if dist2.is_initialized():
+            dist2.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name,K,partition", [
+    (2, "norm_n48_F602", 2, "features"), (3, "hub1000_F65", 2, "features"),
+    (3, "raw_unsorted_dups_F7", 3, "features"), (2, "special_values_F11", 2, "rows"),
+    (2, "norm_n48_F65", 2, "rows"), (3, "norm_n48_F130", 2, "rows"),
+    (2, "hub1000_F130", 2, "cyclic"), (4, "norm_n48_F65", 3, "cyclic"),
+    (2, "isolated_F17", 1, "features")])
+def test_sgc_precompute_under_torchrun_env(tiny_cases, world, name, K, partition):
+    case = tiny_cases[name]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_torchrun_like_worker,
+                         args=(r, world, port, case, K, partition, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, rest) for r, *rest in (q.get(timeout=180) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = case[f"Y{K}"]
+    for r in range(world):
+        out, stable, ws, timed = got[r]
+        assert ws == world and stable and timed
+        assert out.shape == want.shape
+        assert np.array_equal(out.view(np.uint32), want.view(np.uint32)), (partition, r)
+
+
+def test_single_process_is_untouched(monkeypatch):
+    """No torchrun environment, no group: process_group() is None and
+    sgc_precompute stays on one device; SGC_AMD_AUTO_DIST=0 also opts out."""
+    from sgc_amd import multigpu
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    assert multigpu.torchrun_env() is None
+    assert multigpu.process_group(torch.device("cpu")) is None
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("SGC_AMD_AUTO_DIST", "0")
+    assert multigpu.process_group(torch.device("cpu")) is None
+    assert multigpu.torchrun_env() == (0, 2, 0, 2)
+
+
+def test_devices_from_env(monkeypatch):
+    from sgc_amd import multigpu
+    monkeypatch.delenv("SGC_AMD_DEVICES", raising=False)
+    assert multigpu.devices_from_env(0) is None
+    monkeypatch.setenv("SGC_AMD_DEVICES", "2,0,1")
+    assert multigpu.devices_from_env(1) == [1, 2, 0]  # the caller's device first
+    monkeypatch.setenv("SGC_AMD_DEVICES", "0,0,0")    # virtual devices on one GPU
+    assert multigpu.devices_from_env(0) == [0, 0, 0]
+    monkeypatch.setenv("SGC_AMD_DEVICES", "3")
+    assert multigpu.devices_from_env(3) is None
+
+
+def test_partition_name_checked(monkeypatch):
+    from sgc_amd import multigpu
+    monkeypatch.setenv("SGC_AMD_PARTITION", "diagonal")
+    with pytest.raises(ValueError, match="SGC_AMD_PARTITION"):
+        multigpu.partition_name()
+    monkeypatch.delenv("SGC_AMD_PARTITION")
+    assert multigpu.partition_name() == "features"
