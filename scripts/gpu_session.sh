@@ -31,6 +31,10 @@ for s in $STEPS; do
     smoke)  run smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench timeout -k 10 600 python bench.py ${BENCH_ARGS} ;;
     aux)    run aux timeout -k 10 600 python scripts/bench_aux.py ;;
+    narrow) run narrow timeout -k 10 300 python scripts/narrow_pass.py ${NARROW_ARGS} ;;
+    locality) run locality timeout -k 10 400 python scripts/locality_ab.py ${LOCALITY_ARGS} ;;
+    selfl)  run selfl timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --steps 3 \
+                --warmup 1 --no-cpu-baseline ${DIST_ARGS} ;;
     rccl1)  run rccl1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 1 --steps 5 --warmup 2 \
                 --distributed-path --no-cpu-baseline ${DIST_ARGS} ;;

@@ -78,6 +78,20 @@ class _StreamDone:
         torch.cuda.current_stream(self.dev).wait_event(self.ev)
 
 
+class _EventsDone:
+    """wait() = the current stream waits for the given recorded events (the
+    hub-row launches of a split hop, on their own stream)."""
+    __slots__ = ("evs",)
+
+    def __init__(self, evs):
+        self.evs = evs
+
+    def wait(self):
+        cur = torch.cuda.current_stream()
+        for ev in self.evs:
+            cur.wait_event(ev)
+
+
 def _local_copy(full, loc):
     """The all-gather of a one-rank group: a copy on the current stream --
     which may be a comm stream, so on the GPU it returns a handle whose wait()
@@ -498,11 +512,16 @@ class RowPartitionedPropagator:
             for gi, (a, b) in enumerate(groups):
                 if works[gi] is not None:
                     works[gi].wait()  # this hop's input group has arrived (stream wait)
-                loc = self._buf(("local", par, gi), (s.block, b - a), X0)
+                full = self._buf(("full", par, gi), (PB, b - a), X0)
+                # one rank: its block IS the gathered buffer (no exchange copy)
+                loc = (full if s.world_size == 1 else
+                       self._buf(("local", par, gi), (s.block, b - a), X0))
                 ev_l, ev_h = self._compute(src[gi], loc[:s.rows, :src[gi].shape[1]], layout,
                                            split, key=(h, gi))
-                full = self._buf(("full", par, gi), (PB, b - a), X0)
-                new_works.append(self._issue_gather(full, loc, ev_l, ev_h, split))
+                if s.world_size == 1:
+                    new_works.append(_EventsDone([ev_h]) if ev_h is not None else None)
+                else:
+                    new_works.append(self._issue_gather(full, loc, ev_l, ev_h, split))
                 gathered.append(full)
             works, src, layout = new_works, gathered, "gathered"
         if output == "sharded":
@@ -1185,6 +1204,10 @@ class FeaturePartitionedPropagator:
             if w and n:
                 hop(src, 0, n, dst, own, True)
             src, own = dst, True
+        if P == 1:  # one rank: the last hop writes X_K itself, nothing to exchange
+            if w and n:
+                hop(src, 0, n, out, own, False)
+            return out
         if output == "sharded":
             # last hop -> one all-to-all.  Destination block q is rows
             # [q*Bn, (q+1)*Bn) (equal_row_bounds), so ONE launch over all rows
