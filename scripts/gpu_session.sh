@@ -24,7 +24,7 @@ run() {
 }
 for s in $STEPS; do
   case $s in
-    pytest) run pytest timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    pytest) run pytest timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS} ;;
     cyc)    run cyc timeout -k 10 900 python scripts/cyclic_rehearsal.py ${CYC_ARGS} ;;
     feat)   run feat timeout -k 10 400 python scripts/feature_rehearsal.py ${FEAT_ARGS} ;;
     rankwork) run rankwork timeout -k 10 400 python scripts/rank_work.py ;;
@@ -32,6 +32,8 @@ for s in $STEPS; do
     bench)  run bench timeout -k 10 600 python bench.py ${BENCH_ARGS} ;;
     aux)    run aux timeout -k 10 600 python scripts/bench_aux.py ;;
     narrow) run narrow timeout -k 10 300 python scripts/narrow_pass.py ${NARROW_ARGS} ;;
+    ab)     run ab timeout -k 10 400 python scripts/ab_tune.py ${AB_ARGS} ;;
+    ab8)    run ab8 timeout -k 10 300 python scripts/ab_tune.py --widths F --rows 8:0 ${AB_ARGS} ;;
     locality) run locality timeout -k 10 400 python scripts/locality_ab.py ${LOCALITY_ARGS} ;;
     selfl)  run selfl timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --steps 3 \
                 --warmup 1 --no-cpu-baseline ${DIST_ARGS} ;;

@@ -148,6 +148,115 @@ __device__ __forceinline__ void row_chunks_pipe(const int *__restrict__ col,
         if (ok[c]) *reinterpret_cast<VT *>(Yb + boff[c]) = acc[c];
 }
 
+// Heavy row of the multi-row kernel, two nonzeros per load instruction: lanes
+// 0-31 gather nonzero k's X segment, lanes 32-63 nonzero k+1's (16-B lanes,
+// up to 128 floats per half), so one global_load_dwordx4 moves up to 1 KB
+// (a one-row-per-instruction wave moves at most half that, and only the row
+// width -- 304 B at a 76-float feature block).  v_permlane32_swap then gives
+// every lane both values of its features (lo = x_k, hi = x_k+1) and the chain
+// takes them in order, acc = fma(v_k, x_k, acc); acc = fma(v_k+1, x_k+1, acc):
+// the same sequential FMA chain per element as one nonzero at a time (both
+// halves compute it; the low half stores).  U pairs per step, two steps in
+// flight (2U nonzeros each); (col, val) of 64 consecutive nonzeros in one VGPR
+// per lane, the next block loaded one ahead.  Indices past the row clamp to
+// its last nonzero (never out of bounds) and their FMAs are skipped.
+template <int U>
+__device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
+                                               const float *__restrict__ val, int k0, int k1,
+                                               const float *__restrict__ X, int64_t ldx,
+                                               float *__restrict__ yrow, int F, int f_lane,
+                                               bool lane_ok, bool vec_store, int lane,
+                                               bool accum) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    constexpr int kPairs = kWave / (2 * U);  // steps per 64-nonzero block
+    static_assert(kWave % (2 * U) == 0 && kPairs % 2 == 0, "2U must divide 64 into an even count");
+    if (accum && k1 == k0) return;  // nothing to add: the row keeps its partial chains
+    const bool hi = lane >= 32;
+    const uint32_t boff = lane_ok ? uint32_t(f_lane) * 4u : 0u;
+    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (accum && lane_ok) {  // continue the chains an earlier column-block pass stored
+        if (vec_store) {
+            acc = *reinterpret_cast<const f4 *>(yrow + f_lane);
+        } else {
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                if (f_lane + v < F) acc[v] = yrow[f_lane + v];
+        }
+    }
+    if (k1 > k0) {
+        const char *Xb = reinterpret_cast<const char *>(X);
+        const int64_t row_bytes = ldx * 4;
+        const int last = k1 - 1;
+        int colA = ld_meta(col + min(k0 + lane, last));
+        float valA = ld_meta(val + min(k0 + lane, last));
+        int colB = ld_meta(col + min(k0 + kWave + lane, last));
+        float valB = ld_meta(val + min(k0 + kWave + lane, last));
+        f4 xv[2][U];
+        float v0[2][U], v1[2][U];
+        auto issue = [&](int base, int i, int colr, float valr, int buf) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int ka = min(base + i * 2 * U + 2 * u, last);
+                const int kb = min(ka + 1, last);
+                const int la = (ka - base) & (kWave - 1), lb = (kb - base) & (kWave - 1);
+                const int ca = __builtin_amdgcn_readlane(colr, la);
+                const int cb = __builtin_amdgcn_readlane(colr, lb);
+                v0[buf][u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(valr), la));
+                v1[buf][u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(valr), lb));
+                const int cj = hi ? cb : ca;
+                xv[buf][u] = *reinterpret_cast<const f4 *>(Xb + (int64_t)cj * row_bytes + boff);
+            }
+        };
+        issue(k0, 0, colA, valA, 0);
+        for (int base = k0;; base += kWave) {
+#pragma unroll
+            for (int i = 0; i < kPairs; ++i) {
+                const int cur = base + i * 2 * U;
+                if (cur > last) break;  // uniform; the step issued for it is dropped
+                if (i + 1 < kPairs)
+                    issue(base, i + 1, colA, valA, (i + 1) & 1);
+                else  // first step of the next block, from its prefetched (col, val)
+                    issue(base + kWave, 0, colB, valB, 0);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int ka = cur + 2 * u;
+                    if (ka > last) break;  // uniform
+                    f4 xa, xb;
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const uint32_t x = __float_as_uint(xv[i & 1][u][v]);
+                        // [x.lo | x.hi] -> lanes all x_k (lo), all x_k+1 (hi)
+                        const auto t = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+                        xa[v] = __uint_as_float(t[0]);
+                        xb[v] = __uint_as_float(t[1]);
+                    }
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) acc[v] = __builtin_fmaf(v0[i & 1][u], xa[v], acc[v]);
+                    if (ka + 1 <= last) {
+#pragma unroll
+                        for (int v = 0; v < 4; ++v)
+                            acc[v] = __builtin_fmaf(v1[i & 1][u], xb[v], acc[v]);
+                    }
+                }
+            }
+            if (base + kWave > last) break;
+            colA = colB;
+            valA = valB;
+            colB = ld_meta(col + min(base + 2 * kWave + lane, last));
+            valB = ld_meta(val + min(base + 2 * kWave + lane, last));
+        }
+    }
+    if (!hi && lane_ok) {
+        if (vec_store) {
+            *reinterpret_cast<f4 *>(yrow + f_lane) = acc;
+        } else {
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                if (f_lane + v < F) yrow[f_lane + v] = acc[v];
+        }
+    }
+}
+
 // Grid: x = work items of one feature slice, y = slice.  Workgroups are
 // dispatched x-fastest, so the chip sweeps the slices one after another and
 // only X[:, slice] (N x 64CV floats -- 119 MB at Reddit shape for 128
@@ -219,6 +328,7 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 // flight per row; packing heavy rows R per wave like light rows measured 1.7x
 // slower on a 76-float slice, profiles/r02/packed_sweep.log).
 constexpr int kRowsU = 4;  // nonzeros per row per step (one b128 (col, val) read each)
+constexpr int kPairsU = 4;  // heavy rows, pair mode: nonzero pairs per step (8 nonzeros)
 
 template <int LB, int VH, int UH>
 __global__ __launch_bounds__(256) void spmm_rows_kernel(
@@ -226,7 +336,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
     int row_begin, int n_rows, int F, int F_load, int LR, int vec_store, int n_sub,
     const int *__restrict__ heavy_rows, int n_heavy, int heavy_threshold, int accum,
-    const int *__restrict__ light_rows) {
+    const int *__restrict__ light_rows, int heavy_pairs) {
     constexpr int V = 4, U = kRowsU < LB / 2 ? kRowsU : LB / 2;
     constexpr int kSteps = LB / U;  // steps per LDS block
     static_assert(kSteps >= 2 && kSteps % 2 == 0, "bad block");
@@ -242,10 +352,17 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const int n_heavy_items = n_heavy * n_sub;
     if (wave < n_heavy_items) {
         const int h = wave / n_sub;
-        const int sub = slice * n_sub + (wave - h * n_sub);  // in units of 64*VH floats
-        if (sub * kWave * VH >= F) return;
         const int row = heavy_rows[h];
         const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
+        if (heavy_pairs) {  // n_sub == 1: one item per (row, slice), two nonzeros per load
+            const int j = lane & 31;
+            const int f = slice * (LR * V) + j * V;
+            row_pairs_pipe<kPairsU>(col, val, k0, k1, X, ldx, Y + (int64_t)(row - row_begin) * ldy,
+                                    F, f, j < LR && f < F_load, vec_store != 0, lane, accum != 0);
+            return;
+        }
+        const int sub = slice * n_sub + (wave - h * n_sub);  // in units of 64*VH floats
+        if (sub * kWave * VH >= F) return;
         row_chunks_pipe<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
                                         Y + (int64_t)(row - row_begin) * ldy, F, sub, lane,
                                         accum != 0);
@@ -878,13 +995,19 @@ static int g_max_vec = 4;
 // profiles/r02/sweep_rows*.  Set through sgc_set_tuning("rows_per_wave").
 static int g_rows_per_wave = 0;
 
+// Heavy rows of the multi-row kernel: 1 = two nonzeros per load instruction
+// (row_pairs_pipe, 16-B lanes), 0 = one wave per 64*VH-float sub-chunk
+// (row_chunks_pipe).  Set through sgc_set_tuning("heavy_pairs").
+static int g_heavy_pairs = 1;
+
 template <int LB, int VH>
 hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int R = kWave / LR, SW = LR * 4;
     const int slices = (F_load + SW - 1) / SW;
     // heavy sub-chunks per slice (unpacked heavy rows): whole 64*VH-float
     // chunks of a slice, or of the launch's width when it is a single slice
-    const int n_sub = slices > 1 ? SW / (kWave * VH) : (F_load + kWave * VH - 1) / (kWave * VH);
+    const int n_sub = g_heavy_pairs ? 1
+                      : slices > 1 ? SW / (kWave * VH) : (F_load + kWave * VH - 1) / (kWave * VH);
     const int64_t heavy_waves = (int64_t)a.n_heavy * n_sub;
     // light items: every row (non-light rows skip themselves), or with a
     // light order exactly the light rows
@@ -895,7 +1018,7 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
                        n_light_items, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
-                       a.heavy_threshold, a.accum, a.light_rows);
+                       a.heavy_threshold, a.accum, a.light_rows, g_heavy_pairs);
     return hipGetLastError();
 }
 
@@ -965,6 +1088,11 @@ int set_tuning(const char *key, int64_t value) {
         g_rows_per_wave = (int)value;
         return SGC_OK;
     }
+    if (std::string(key) == "heavy_pairs") {
+        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "heavy_pairs must be 0 or 1");
+        g_heavy_pairs = (int)value;
+        return SGC_OK;
+    }
     if (std::string(key) == "max_vec") {
         SGC_REQUIRE(value == 1 || value == 2 || value == 4, SGC_EINVAL, "max_vec must be 1, 2 or 4");
         g_max_vec = (int)value;
@@ -977,6 +1105,7 @@ int set_tuning(const char *key, int64_t value) {
 int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "slice_floats") return g_slice_floats;
     if (key && std::string(key) == "max_vec") return g_max_vec;
+    if (key && std::string(key) == "heavy_pairs") return g_heavy_pairs;
     if (key && std::string(key) == "rows_per_wave") return g_rows_per_wave;
     if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
     if (key && std::string(key) == "hub_stream") return g_hub_stream;
