@@ -48,7 +48,7 @@ def main():
         b = nnz_balanced_bounds(S.row_ptr, P)
         r0, r1 = int(b[p]), int(b[p + 1])
     for wspec in args.widths.split(","):
-        if wspec == "F":
+        if wspec == "F" and args.rows == "all":
             out = torch.empty_like(X)
 
             def run():
@@ -56,7 +56,7 @@ def main():
                 return out
             label = f"{args.shape} propagate K={K} (F={F})"
         else:
-            w = int(wspec)
+            w = F if wspec == "F" else int(wspec)
             ld = (w + 31) // 32 * 32
             Xw = torch.zeros((S.n, ld), device=dev)
             Xw[:, :w] = X[:, :w]
