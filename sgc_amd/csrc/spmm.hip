@@ -160,6 +160,8 @@ __device__ __forceinline__ void row_chunks_pipe(const int *__restrict__ col,
 // flight (2U nonzeros each); (col, val) of 64 consecutive nonzeros in one VGPR
 // per lane, the next block loaded one ahead.  Indices past the row clamp to
 // its last nonzero (never out of bounds) and their FMAs are skipped.
+constexpr int kPairsU = 4;  // nonzero pairs per step (8 nonzeros; 16 in flight)
+
 template <int U>
 __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
                                                const float *__restrict__ val, int k0, int k1,
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
     int row_begin, int n_rows, int F, const int *__restrict__ heavy_rows, int n_heavy,
-    int heavy_threshold, int accum) {
+    int heavy_threshold, int accum, int heavy_pairs) {
     constexpr int VH = (SGC_HEAVY_VEC < V) ? SGC_HEAVY_VEC : V;  // heavy lanes' vector width
     constexpr int kSub = C * V / VH;  // 64*VH-float sub-chunks per slice (heavy items)
     const int lane = threadIdx.x & (kWave - 1);
@@ -287,6 +289,15 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
         if (sub * kWave * VH >= F) return;
         const int row = heavy_rows[h];
         const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
+        if constexpr (V == 4 && VH == 2) {
+            if (heavy_pairs) {  // the same 128-float sub-chunk, two nonzeros per load
+                const int f = sub * 128 + (lane & 31) * 4;
+                row_pairs_pipe<kPairsU>(col, val, k0, k1, X, ldx,
+                                        Y + (int64_t)(row - row_begin) * ldy, F, f, f < F, true,
+                                        lane, accum != 0);
+                return;
+            }
+        }
         row_chunks_pipe<VH, 1, UH / VH>(col, val, k0, k1, X, ldx,
                                         Y + (int64_t)(row - row_begin) * ldy, F, sub, lane,
                                         accum != 0);
@@ -328,7 +339,6 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 // flight per row; packing heavy rows R per wave like light rows measured 1.7x
 // slower on a 76-float slice, profiles/r02/packed_sweep.log).
 constexpr int kRowsU = 4;  // nonzeros per row per step (one b128 (col, val) read each)
-constexpr int kPairsU = 4;  // heavy rows, pair mode: nonzero pairs per step (8 nonzeros)
 
 template <int LB, int VH, int UH>
 __global__ __launch_bounds__(256) void spmm_rows_kernel(
@@ -959,6 +969,11 @@ struct TimedGuard {
 // vs. an unpipelined U = 16 / 32; profiles/r01_sweep_pipe.log).
 constexpr int kHeavyU = 16;
 
+// Heavy rows (both light kernels; the one-row kernel with 16-B lanes): 1 = two nonzeros per load instruction
+// (row_pairs_pipe, 16-B lanes), 0 = one wave per 64*VH-float sub-chunk
+// (row_chunks_pipe).  Set through sgc_set_tuning("heavy_pairs").
+static int g_heavy_pairs = 1;
+
 template <int V, int C>
 hipError_t launch_vc(const LaunchArgs &a) {
     constexpr int U0 = (C * V >= 16) ? 2 : (C * V >= 8) ? 4 : 8;
@@ -970,7 +985,7 @@ hipError_t launch_vc(const LaunchArgs &a) {
     dim3 grid((unsigned)blocks, (unsigned)a.slices);
     hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin, a.n_rows,
-                       a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold, a.accum);
+                       a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold, a.accum, g_heavy_pairs);
     return hipGetLastError();
 }
 
@@ -994,11 +1009,6 @@ static int g_max_vec = 4;
 // spmm_rows_kernel with 32 / 16 lanes per row on wide launches; 1 = never.
 // profiles/r02/sweep_rows*.  Set through sgc_set_tuning("rows_per_wave").
 static int g_rows_per_wave = 0;
-
-// Heavy rows of the multi-row kernel: 1 = two nonzeros per load instruction
-// (row_pairs_pipe, 16-B lanes), 0 = one wave per 64*VH-float sub-chunk
-// (row_chunks_pipe).  Set through sgc_set_tuning("heavy_pairs").
-static int g_heavy_pairs = 1;
 
 template <int LB, int VH>
 hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
