@@ -336,6 +336,20 @@ int sgc_propagate_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const 
                           int64_t ldo, int64_t F, int32_t K, void *workspace,
                           int64_t workspace_bytes, int32_t n_threads);
 
+/* The whole launch plan in one call, on the device: plan[0 .. n) = every row
+ * of [row_begin, row_end) sorted by degree, longest first, ties in ascending
+ * row order (a stable radix sort) -- i.e. the heavy rows (degree > threshold)
+ * heaviest first followed by the light rows in SGC_SPMM_LIGHT_ORDER order,
+ * exactly what sgc_plan_build + sgc_plan_light_order write together.
+ * counts_host[0] = rows above threshold (n_heavy), [1] = rows above
+ * hub_threshold (n_hub), [2] = the longest row's nonzeros.  One stream
+ * synchronisation (the counts); workspace of sgc_plan_sorted_workspace(n)
+ * bytes on the device.  Replaces nothing in the reference (a schedule). */
+int64_t sgc_plan_sorted_workspace(int64_t n_rows);
+int sgc_plan_sorted(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
+                    int32_t threshold, int32_t hub_threshold, int32_t *plan, void *workspace,
+                    int64_t workspace_bytes, int64_t *counts_host, void *stream);
+
 /* ---------------------------------------------------------------------------
  * One process, several GPUs (the multi-GPU form of the one
  * call reddit.py:43 makes, sgc_precompute -> utils.py:92-97).  The engine

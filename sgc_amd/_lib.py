@@ -67,6 +67,8 @@ SIGNATURES = {
     "sgc_propagate_cpu_workspace": (_i64, [_i64, _i64, _i32]),
     "sgc_propagate_f32_cpu": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _i32,
                                              _p, _i64, _i32]),
+    "sgc_plan_sorted_workspace": (_i64, [_i64]),
+    "sgc_plan_sorted": (ctypes.c_int, [_p, _i64, _i64, _i32, _i32, _p, _p, _i64, _p, _p]),
     "sgc_mgpu_init": (ctypes.c_int, [ctypes.c_int, _p]),
     "sgc_mgpu_attach": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _p, ctypes.POINTER(_i64)]),
     "sgc_mgpu_propagate": (ctypes.c_int, [_i64, _p, _i64, _p, _i64, _i64, _i32, _p]),

@@ -73,6 +73,10 @@ int propagate_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *v
                   int32_t K, void *workspace, int64_t workspace_bytes, int32_t n_threads);
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                       int64_t ldy, int64_t M, int64_t K, int64_t C, hipStream_t stream);
+int64_t plan_sorted_workspace(int64_t n_rows);
+int plan_sorted(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int32_t threshold,
+                int32_t hub_threshold, int32_t *plan, void *workspace, int64_t workspace_bytes,
+                int64_t *counts_host, hipStream_t stream);
 int mgpu_init(int ndev, const int *devices);
 int mgpu_finalize();
 int mgpu_attach(const int32_t *row_ptr, const int32_t *col_idx, const float *val, int64_t n,
@@ -355,3 +359,12 @@ int sgc_mgpu_propagate(int64_t handle, const float *X0, int64_t ldx, float *out,
 int sgc_mgpu_detach(int64_t handle) { return mgpu_detach(handle); }
 
 int sgc_mgpu_finalize(void) { return mgpu_finalize(); }
+
+int64_t sgc_plan_sorted_workspace(int64_t n_rows) { return plan_sorted_workspace(n_rows); }
+
+int sgc_plan_sorted(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
+                    int32_t threshold, int32_t hub_threshold, int32_t *plan, void *workspace,
+                    int64_t workspace_bytes, int64_t *counts_host, void *stream) {
+    return plan_sorted(row_ptr, row_begin, row_end, threshold, hub_threshold, plan, workspace,
+                       workspace_bytes, counts_host, as_stream(stream));
+}

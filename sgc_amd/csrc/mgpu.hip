@@ -33,11 +33,10 @@
 
 namespace sgc {
 
-int build_plan(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int32_t threshold,
-               int32_t hub_threshold, int32_t *plan, int64_t capacity, int64_t *n_heavy_host,
-               int64_t *n_hub_host, hipStream_t stream);
-int light_order(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int32_t threshold,
-                int32_t *light, int64_t *n_light_host, hipStream_t stream);
+int64_t plan_sorted_workspace(int64_t n_rows);
+int plan_sorted(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int32_t threshold,
+                int32_t hub_threshold, int32_t *plan, void *workspace, int64_t workspace_bytes,
+                int64_t *counts_host, hipStream_t stream);
 int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                 int64_t row_begin, int64_t row_end, const float *X, int64_t ldx, float *Y,
                 int64_t ldy, int64_t F, const int32_t *heavy_rows, int64_t n_heavy,
@@ -176,30 +175,21 @@ int plan_for(Graph &g, Replica &r, int64_t width, hipStream_t stream, const Plan
     }
     Plan p;
     p.threshold = th;
-    const int64_t cap = 2 * g.n + 1;
-    SGC_HIP_CHECK(hipMalloc(&p.rows, (size_t)std::max<int64_t>(cap, g.n) * sizeof(int32_t)));
-    int rc = build_plan(r.row_ptr, 0, g.n, th, hub, p.rows, cap, &p.n_heavy, &p.n_hub, stream);
+    SGC_HIP_CHECK(hipMalloc(&p.rows, (size_t)std::max<int64_t>(1, g.n) * sizeof(int32_t)));
+    const int64_t ws_bytes = plan_sorted_workspace(g.n);
+    void *ws = nullptr;
+    SGC_HIP_CHECK(hipMalloc(&ws, (size_t)ws_bytes));
+    int64_t counts[3] = {0, 0, 0};
+    int rc = plan_sorted(r.row_ptr, 0, g.n, th, hub, p.rows, ws, ws_bytes, counts, stream);
+    (void)hipFree(ws);  // plan_sorted synchronised the stream
     if (rc != SGC_OK) {
         (void)hipFree(p.rows);
         return rc;
     }
-    if (p.n_hub > 0) {  // heaviest first: plan row 0 is the longest hub chain
-        int32_t row = 0, ends[2] = {0, 0};
-        SGC_HIP_CHECK(hipMemcpy(&row, p.rows, sizeof(int32_t), hipMemcpyDeviceToHost));
-        SGC_HIP_CHECK(hipMemcpy(ends, r.row_ptr + row, 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
-        if (ends[1] - ends[0] <= kHubSerialMaxDegree) p.flags |= SGC_SPMM_HUB_SERIAL;
-    }
-    if (g.n > p.n_heavy) {
-        int64_t n_light = 0;
-        rc = light_order(r.row_ptr, 0, g.n, th, p.rows + p.n_heavy, &n_light, stream);
-        if (rc != SGC_OK) {
-            (void)hipFree(p.rows);
-            return rc;
-        }
-        SGC_REQUIRE(n_light == g.n - p.n_heavy, SGC_EINVAL,
-                    "mgpu: light order does not cover the light rows");
-        p.flags |= SGC_SPMM_LIGHT_ORDER;
-    }
+    p.n_heavy = counts[0];
+    p.n_hub = counts[1];
+    if (p.n_hub > 0 && counts[2] <= kHubSerialMaxDegree) p.flags |= SGC_SPMM_HUB_SERIAL;
+    if (g.n > p.n_heavy) p.flags |= SGC_SPMM_LIGHT_ORDER;
     *out = &(r.plans[{th, hub}] = p);
     return SGC_OK;
 }

@@ -259,6 +259,8 @@ class DeviceCSR:
             hub = auto_hub_threshold(self.range_nnz(row_begin, row_end), threshold)
         hub = max(hub, threshold)
         key = (row_begin, row_end, threshold, hub)
+        if key not in self._plans and LIGHT_ORDER and self.device.type == "cuda":
+            self._plans[key] = self._plan_sorted(row_begin, row_end, threshold, hub)
         if key not in self._plans:
             lib = _lib.load()
             n = row_end - row_begin
@@ -292,6 +294,26 @@ class DeviceCSR:
                 ordered = True
             self._plans[key] = Plan(rows, h, nh, threshold, deg, ordered)
         return self._plans[key]
+
+
+    def _plan_sorted(self, row_begin, row_end, threshold, hub):
+        """The plan from one device radix sort (sgc_plan_sorted): all rows of
+        the range by degree, longest first -- heavy rows, then the light rows
+        in processing order -- and the counts in one read-back."""
+        import ctypes
+        lib = _lib.load()
+        n = row_end - row_begin
+        rows = torch.empty(max(1, n), dtype=torch.int32, device=self.device)
+        ws_bytes = lib.sgc_plan_sorted_workspace(n)
+        ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8, device=self.device)
+        counts = (ctypes.c_int64 * 3)()
+        with torch.cuda.device(self.device):
+            _lib.check(lib.sgc_plan_sorted(_lib.ptr(self.row_ptr), row_begin, row_end, threshold,
+                                           hub, _lib.ptr(rows), _lib.ptr(ws), ws_bytes,
+                                           ctypes.cast(counts, ctypes.c_void_p),
+                                           _lib.stream_handle(self.device)), "plan_sorted")
+        h, nh = int(counts[0]), int(counts[1])
+        return Plan(rows, h, nh, threshold, int(counts[2]) if nh > 0 else 0, n > h)
 
 
 def to_torch_coo(csr: DeviceCSR):

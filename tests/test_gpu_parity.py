@@ -593,3 +593,31 @@ def test_plan_light_order(r0, r1, th):
     want = (light[np.argsort(-d[light], kind="stable")] + r0).astype(np.int32)
     assert n.value == len(want)
     assert np.array_equal(out[:n.value].cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("r0,r1,th,hub", [(0, 4000, 7, 15), (123, 3001, 0, 0), (0, 4000, 30, 30),
+                                          (50, 50, 5, 9), (7, 4000, 2**31 - 2, 2**31 - 2)])
+def test_plan_sorted_matches_host_plan(r0, r1, th, hub):
+    """sgc_plan_sorted (one device radix sort) lists every row of the range by
+    degree, longest first, ties in row order -- the heavy rows of
+    sgc_plan_build followed by the light order of sgc_plan_light_order -- and
+    counts the heavy rows, the hub rows and the longest row."""
+    import ctypes
+    from sgc_amd import _lib
+    rng = np.random.default_rng(r0 + r1 + th)
+    deg = rng.integers(0, 40, 4000)
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    rp_d = torch.from_numpy(rp).to(DEV)
+    n = r1 - r0
+    lib = _lib.load()
+    out = torch.full((max(1, n),), -1, dtype=torch.int32, device=DEV)
+    wb = lib.sgc_plan_sorted_workspace(n)
+    ws = torch.empty(max(1, wb), dtype=torch.uint8, device=DEV)
+    counts = (ctypes.c_int64 * 3)()
+    _lib.check(lib.sgc_plan_sorted(_lib.ptr(rp_d), r0, r1, th, hub, _lib.ptr(out), _lib.ptr(ws), wb,
+                                   ctypes.cast(counts, ctypes.c_void_p), _lib.stream_handle(DEV)),
+               "plan_sorted")
+    d = deg[r0:r1]
+    want = (np.argsort(-d, kind="stable") + r0).astype(np.int32)
+    assert list(counts) == [int((d > th).sum()), int((d > hub).sum()), int(d.max()) if n else 0]
+    assert np.array_equal(out[:n].cpu().numpy(), want)
