@@ -18,12 +18,14 @@ call) is one "launch"; the JSON holds the mean bytes per launch.
 
 Calibration (MI355X_MICROARCH.md, HBM section: FETCH_SIZE under-counts wide
 coalesced reads on gfx950 and other widths are uncalibrated): the workload
-first runs the SAME kernel over an identity S (N_cal rows, one nonzero each)
-at the shape's feature width and row layout, which reads every X row exactly
-once with the kernel's own gathers and writes every Y row once -- a known
-byte count far beyond the 256 MiB Infinity Cache.  read_factor =
-known_read_bytes / FETCH_SIZE bytes of that launch is then applied to the
-shape's launches.  FETCH_SIZE counts Infinity-Cache hits (the guide), so the
+first runs the SAME kernel over a random PERMUTATION S (N_cal rows, one
+nonzero each, columns a seeded random permutation) at the shape's feature
+width and row layout -- the gather pattern of the real hops, each X row read
+exactly once in random order, each Y row written once: a known byte count
+far beyond the 256 MiB Infinity Cache.  read_factor = known_read_bytes /
+FETCH_SIZE bytes of that launch is then applied to the shape's launches.
+The identity S (rows in order: a streaming pattern, the round-2
+calibration) is run too and its factor reported beside it.  FETCH_SIZE counts Infinity-Cache hits (the guide), so the
 result is the traffic beyond L2: an upper bound on HBM bytes.
 
 The record carries the sha256 of the libsgc_amd.so it was taken with and the
@@ -42,7 +44,7 @@ sys.path.insert(0, ROOT)
 
 N_CAL = 1_000_000
 REPEATS = 3
-TUNING_KEYS = ("slice_floats", "max_vec", "hub_chunk", "hub_first", "hub_priority")
+TUNING_KEYS = ("slice_floats", "max_vec", "hub_chunk", "heavy_pairs", "rows_per_wave")
 
 
 def lib_sha():
@@ -71,17 +73,20 @@ def workload(shape):
         v = os.environ.get("SGC_PMC_" + key.upper())
         if v is not None:
             lib.sgc_set_tuning(key.encode(), int(v))
-    # calibration: identity S, X row i read once, Y row i written once
+    # calibration: identity S (streaming), then a random permutation S (the
+    # gather pattern); each X row read once, each Y row written once
     rp = np.arange(N_CAL + 1, dtype=np.int32)
-    ci = np.arange(N_CAL, dtype=np.int32)
     va = np.ones(N_CAL, dtype=np.float32)
-    cal = DeviceCSR.from_host_arrays(rp, ci, va, device=dev)
     Xc = torch.randn((N_CAL, LD), device=dev)[:, :F]
     Yc = torch.empty((N_CAL, LD), device=dev)[:, :F]
-    for _ in range(REPEATS):  # the padded-buffer flags select the kernel the hops use
-        spmm(cal, Xc, out=Yc, use_plan=False, flags=SPMM_X_PADDED | SPMM_Y_PADDED)
-    torch.cuda.synchronize()
-    del Xc, Yc, cal
+    for ci in (np.arange(N_CAL, dtype=np.int32),
+               np.random.default_rng(7).permutation(N_CAL).astype(np.int32)):
+        cal = DeviceCSR.from_host_arrays(rp, ci, va, device=dev)
+        for _ in range(REPEATS):  # the padded-buffer flags select the kernel the hops use
+            spmm(cal, Xc, out=Yc, use_plan=False, flags=SPMM_X_PADDED | SPMM_Y_PADDED)
+        torch.cuda.synchronize()
+        del cal
+    del Xc, Yc
     S = graphs.synthetic_graph(shape, seed=0)
     X0 = torch.from_numpy(graphs.synthetic_features(shape, S.n, F, seed=1)).to(dev)
     csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
@@ -135,13 +140,15 @@ def _per_dispatch(rows, counter):
 
 
 def _launches(d, K):
-    """(calibration dispatch ids, [[main id, hub ids...] per shape launch])."""
+    """(identity-calibration ids, permutation-calibration ids,
+    [[main id, hub ids...] per shape launch])."""
     ks = sorted(k for k, (nm, _) in d.items()
                 if "spmm_csr_kernel" in nm or "spmm_rows_kernel" in nm)
     hubs = sorted(k for k, (nm, _) in d.items() if "spmm_hub_kernel" in nm)
-    cal, main = ks[:REPEATS], ks[REPEATS:REPEATS + REPEATS * K]
-    prev = [cal[-1]] + main[:-1]
-    return cal, [[k] + [h for h in hubs if p < h < k] for p, k in zip(prev, main)]
+    cal_id, cal_perm = ks[:REPEATS], ks[REPEATS:2 * REPEATS]
+    main = ks[2 * REPEATS:2 * REPEATS + REPEATS * K]
+    prev = [cal_perm[-1]] + main[:-1]
+    return cal_id, cal_perm, [[k] + [h for h in hubs if p < h < k] for p, k in zip(prev, main)]
 
 
 def summarize(out_dir, shape):
@@ -152,9 +159,9 @@ def summarize(out_dir, shape):
     write = _per_dispatch(_rows(os.path.join(out_dir, "pmc_write")), "WRITE_SIZE")
     l2 = _rows(os.path.join(out_dir, "pmc_l2"))
     hit, miss = _per_dispatch(l2, "TCC_HIT_sum"), _per_dispatch(l2, "TCC_MISS_sum")
-    cal_f, red_f = _launches(fetch, K)
-    cal_w, red_w = _launches(write, K)
-    _, red_h = _launches(hit, K)
+    calid_f, cal_f, red_f = _launches(fetch, K)
+    calid_w, cal_w, red_w = _launches(write, K)
+    _, _, red_h = _launches(hit, K)
 
     def mean(d, ks):
         vals = [sum(d[j][1] for j in k) if isinstance(k, list) else d[k][1] for k in ks]
@@ -166,6 +173,8 @@ def summarize(out_dir, shape):
     cal_write_b = mean(write, cal_w) * 1024
     read_factor = known_read / cal_fetch_b
     write_factor = known_write / cal_write_b
+    id_read_factor = known_read / (mean(fetch, calid_f) * 1024)
+    id_write_factor = known_write / (mean(write, calid_w) * 1024)
     red_fetch_b = mean(fetch, red_f) * 1024 * read_factor
     red_write_b = mean(write, red_w) * 1024 * write_factor
     h, m = mean(hit, red_h), mean(miss, red_h)
@@ -182,11 +191,14 @@ def summarize(out_dir, shape):
         "hbm_read_bytes_per_launch": red_fetch_b,
         "hbm_write_bytes_per_launch": red_write_b,
         "raw_FETCH_SIZE_kB": mean(fetch, red_f), "raw_WRITE_SIZE_kB": mean(write, red_w),
-        "calibration": {"kernel": f"same spmm kernel over identity S, F={F}, ld {LD}",
+        "calibration": {"kernel": f"same spmm kernel over a random permutation S (each X "
+                                  f"row gathered once, random order), F={F}, ld {LD}",
                         "rows": n_cal, "known_read_bytes": known_read,
                         "known_write_bytes": known_write, "FETCH_SIZE_bytes": cal_fetch_b,
                         "WRITE_SIZE_bytes": cal_write_b, "read_factor": read_factor,
-                        "write_factor": write_factor},
+                        "write_factor": write_factor,
+                        "identity_S_read_factor": id_read_factor,
+                        "identity_S_write_factor": id_write_factor},
         "l2_hit_rate": h / (h + m) if (h + m) > 0 and not math.isnan(h) else None,
         "kernel_ms": (sum(main_ms) / len(main_ms)) if main_ms else None,
         "kernel_ms_note": "spmm_csr_kernel mean duration in the profiled FETCH_SIZE pass "
