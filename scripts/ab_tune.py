@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--widths", default="F,76")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--rows", default="all", help="all, or P:p = rank p's 1/P nnz-balanced rows")
+    ap.add_argument("--kwarg", default=None,
+                    help="A/B a keyword of spmm() (threshold, hub_threshold) instead of a knob; "
+                         "-1 = the default")
     args = ap.parse_args()
     lib = _lib.load()
     dev = torch.device("cuda", 0)
@@ -47,6 +50,7 @@ def main():
         P, p = (int(x) for x in args.rows.split(":"))
         b = nnz_balanced_bounds(S.row_ptr, P)
         r0, r1 = int(b[p]), int(b[p + 1])
+    cur = {"v": -1}
     for wspec in args.widths.split(","):
         if wspec == "F" and args.rows == "all":
             out = torch.empty_like(X)
@@ -63,18 +67,28 @@ def main():
             Y = torch.empty((r1 - r0, ld), device=dev)
 
             def run(Xw=Xw, Y=Y, w=w):
-                spmm(csr, Xw[:, :w], r0, r1, out=Y[:, :w], flags=SPMM_X_PADDED | SPMM_Y_PADDED)
+                kw = {}
+                if args.kwarg and cur["v"] >= 0:
+                    kw[args.kwarg] = cur["v"]
+                spmm(csr, Xw[:, :w], r0, r1, out=Y[:, :w], flags=SPMM_X_PADDED | SPMM_Y_PADDED,
+                     **kw)
                 return Y[:, :w]
             label = f"one hop, width {w}, rows [{r0}, {r1})"
         ms = {v: [] for v in values}
         outs = {}
+
+        def select(v):
+            if args.kwarg:
+                cur["v"] = v
+            else:
+                _lib.check(lib.sgc_set_tuning(args.knob.encode(), v), "set_tuning")
         for v in values:  # warm-up: plans, code objects
-            _lib.check(lib.sgc_set_tuning(args.knob.encode(), v), "set_tuning")
+            select(v)
             outs[v] = run().clone()
         torch.cuda.synchronize()
         for _ in range(args.rounds):
             for v in values:
-                _lib.check(lib.sgc_set_tuning(args.knob.encode(), v), "set_tuning")
+                select(v)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 run()
@@ -82,7 +96,7 @@ def main():
                 torch.cuda.synchronize()
                 ms[v].append(s.elapsed_time(e))
         same = all(torch.equal(outs[v], outs[values[0]]) for v in values)
-        rec = {"case": label, "knob": args.knob, "bit_identical": bool(same)}
+        rec = {"case": label, "knob": args.kwarg or args.knob, "bit_identical": bool(same)}
         for v in values:
             rec[f"{v}_median_ms"] = round(float(np.median(ms[v])), 4)
             rec[f"{v}_min_ms"] = round(float(np.min(ms[v])), 4)

@@ -40,7 +40,10 @@ class LocalCyclic(CyclicRowPropagator):
     """Compute-only: the exchange is skipped."""
 
     def _all_gather(self, full, loc):
-        return None
+        # no copy (the exchange is modelled), but the consumer still waits for
+        # the work enqueued on the comm stream so far, as RCCL's wait() would
+        from sgc_amd.distributed import _StreamDone
+        return _StreamDone(torch.cuda.current_stream(full.device)) if full.is_cuda else None
 
 
 def timeit(fn, reps=10, warm=3):

@@ -33,7 +33,7 @@ for s in $STEPS; do
     aux)    run aux timeout -k 10 600 python scripts/bench_aux.py ;;
     narrow) run narrow timeout -k 10 300 python scripts/narrow_pass.py ${NARROW_ARGS} ;;
     ab)     run ab timeout -k 10 400 python scripts/ab_tune.py ${AB_ARGS} ;;
-    ab8)    run ab8 timeout -k 10 300 python scripts/ab_tune.py --widths F --rows 8:0 ${AB_ARGS} ;;
+    ab8)    run ab8 timeout -k 10 300 python scripts/ab_tune.py --widths F --rows 8:0 ${AB8_ARGS:-$AB_ARGS} ;;
     locality) run locality timeout -k 10 400 python scripts/locality_ab.py ${LOCALITY_ARGS} ;;
     selfl)  run selfl timeout -k 10 400 python bench.py --gpus 2 --dist-backend gloo --steps 3 \
                 --warmup 1 --no-cpu-baseline ${DIST_ARGS} ;;

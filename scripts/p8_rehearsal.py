@@ -46,9 +46,12 @@ class LocalRowPropagator(RowPartitionedPropagator):
     rank's block (compute-only rehearsal on one GPU)."""
 
     def _all_gather(self, full, loc):
+        # the copy runs on the current (comm) stream: hand back a handle whose
+        # wait() orders the consumer after it, like RCCL's work object
+        from sgc_amd.distributed import _StreamDone
         s = self.shard
         full[s.rank * loc.shape[0]:(s.rank + 1) * loc.shape[0]].copy_(loc)
-        return None
+        return _StreamDone(torch.cuda.current_stream(full.device)) if full.is_cuda else None
 
 
 def timeit(fn, reps=10, warm=3):
