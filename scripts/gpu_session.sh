@@ -31,6 +31,8 @@ for s in $STEPS; do
     smoke)  run smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench timeout -k 10 600 python bench.py ${BENCH_ARGS} ;;
     aux)    run aux timeout -k 10 600 python scripts/bench_aux.py ;;
+    hostov) run hostov timeout -k 10 300 python scripts/host_overhead.py ;;
+    ab2)    run ab2 timeout -k 10 400 python scripts/ab_tune.py ${AB2_ARGS} ;;
     narrow) run narrow timeout -k 10 300 python scripts/narrow_pass.py ${NARROW_ARGS} ;;
     ab)     run ab timeout -k 10 400 python scripts/ab_tune.py ${AB_ARGS} ;;
     ab8)    run ab8 timeout -k 10 300 python scripts/ab_tune.py --widths F --rows 8:0 ${AB8_ARGS:-$AB_ARGS} ;;

@@ -969,9 +969,10 @@ struct TimedGuard {
 // vs. an unpipelined U = 16 / 32; profiles/r01_sweep_pipe.log).
 constexpr int kHeavyU = 16;
 
-// Heavy rows (both light kernels; the one-row kernel with 16-B lanes): 1 = two nonzeros per load instruction
-// (row_pairs_pipe, 16-B lanes), 0 = one wave per 64*VH-float sub-chunk
-// (row_chunks_pipe).  Set through sgc_set_tuning("heavy_pairs").
+// Heavy rows, two nonzeros per load instruction (row_pairs_pipe, 16-B lanes)
+// instead of one wave per 64*VH-float sub-chunk (row_chunks_pipe): bit 0 = in
+// the multi-row kernel (Reddit shape K=2: 9.29 -> 9.12 ms, profiles/r03/s1/ab.log),
+// bit 1 = in the one-row kernel.  Set through sgc_set_tuning("heavy_pairs").
 static int g_heavy_pairs = 1;
 
 template <int V, int C>
@@ -985,7 +986,8 @@ hipError_t launch_vc(const LaunchArgs &a) {
     dim3 grid((unsigned)blocks, (unsigned)a.slices);
     hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin, a.n_rows,
-                       a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold, a.accum, g_heavy_pairs);
+                       a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold, a.accum,
+                       (g_heavy_pairs >> 1) & 1);
     return hipGetLastError();
 }
 
@@ -1016,7 +1018,7 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int slices = (F_load + SW - 1) / SW;
     // heavy sub-chunks per slice (unpacked heavy rows): whole 64*VH-float
     // chunks of a slice, or of the launch's width when it is a single slice
-    const int n_sub = g_heavy_pairs ? 1
+    const int n_sub = (g_heavy_pairs & 1) ? 1
                       : slices > 1 ? SW / (kWave * VH) : (F_load + kWave * VH - 1) / (kWave * VH);
     const int64_t heavy_waves = (int64_t)a.n_heavy * n_sub;
     // light items: every row (non-light rows skip themselves), or with a
@@ -1028,7 +1030,7 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
                        n_light_items, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
-                       a.heavy_threshold, a.accum, a.light_rows, g_heavy_pairs);
+                       a.heavy_threshold, a.accum, a.light_rows, g_heavy_pairs & 1);
     return hipGetLastError();
 }
 
@@ -1099,7 +1101,7 @@ int set_tuning(const char *key, int64_t value) {
         return SGC_OK;
     }
     if (std::string(key) == "heavy_pairs") {
-        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "heavy_pairs must be 0 or 1");
+        SGC_REQUIRE(value >= 0 && value <= 3, SGC_EINVAL, "heavy_pairs must be 0..3 (a bit mask)");
         g_heavy_pairs = (int)value;
         return SGC_OK;
     }

@@ -364,14 +364,18 @@ class RowPartitionedPropagator:
         hub_s = self._hub_stream(key[-1] if isinstance(key[-1], int) else 0, X.device)
         ready, ev_l, ev_h = self._events(key)
         ready.record(main)
-        if n_rows:
-            self.spmm_fn(self.shard, X, out, layout, "light", **kw)
-        ev_l.record(main)
+        # hub rows first: their CU-sized workgroups must be queued before the
+        # light launch fills every CU, or their ~0.3 ms chains start only as
+        # the light kernel drains and end past it (+0.3 ms per hop at world 1,
+        # profiles/r03 rccl1 logs) -- launch_spmm's own fork orders them so too
         hub_s.wait_event(ready)
         with torch.cuda.stream(hub_s):
             if n_rows:
                 self.spmm_fn(self.shard, X, out, layout, "hub", **kw)
         ev_h.record(hub_s)
+        if n_rows:
+            self.spmm_fn(self.shard, X, out, layout, "light", **kw)
+        ev_l.record(main)
         return ev_l, ev_h
 
     def _issue_gather(self, full, loc, ev_l, ev_h, split):
