@@ -27,6 +27,7 @@ for s in $STEPS; do
     pytest) run pytest timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS} ;;
     cyc)    run cyc timeout -k 10 900 python scripts/cyclic_rehearsal.py ${CYC_ARGS} ;;
     feat)   run feat timeout -k 10 400 python scripts/feature_rehearsal.py ${FEAT_ARGS} ;;
+    p8)     run p8 timeout -k 10 600 python scripts/p8_rehearsal.py ${P8_ARGS} ;;
     rankwork) run rankwork timeout -k 10 400 python scripts/rank_work.py ;;
     smoke)  run smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  run bench timeout -k 10 600 python bench.py ${BENCH_ARGS} ;;
