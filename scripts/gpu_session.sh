@@ -56,6 +56,7 @@ for s in $STEPS; do
             done ;;
     rdist)  run rdist timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                 --master-addr 127.0.0.1 --master-port 29536 drivers/reddit_dist.py --check --test ;;
+    ndiag)  run ndiag bash "$ROOTDIR/scripts/narrow_diag.sh" ;;
     pmc)    for sh in ${PMC_SHAPES:-reddit rmat}; do
               run pmc_$sh env PMC_SHAPE=$sh bash "$ROOTDIR/scripts/pmc_session.sh"
             done ;;
