@@ -241,10 +241,13 @@ int sgc_timing_collect_ex(float *light_ms_host, float *hub_ms_host, float *span_
  * the range, in the order the light rows are to be processed (the Python
  * layer sorts them by length, so the rows sharing a wavefront in the
  * multi-row kernel have about the same length and few lanes idle-load past
- * their row's end).  A schedule only: results never depend on it. */
+ * their row's end).  A schedule only: results never depend on it.
+ * SGC_SPMM_X_UNDER_4G: the caller vouches that every X row a column id can
+ * name lies within 4 GiB of X (n_cols * ldx * 4 < 2^32), so the gathers may
+ * use 32-bit row offsets (fewer address instructions per nonzero).  */
 enum { SGC_SPMM_X_PADDED = 1, SGC_SPMM_Y_PADDED = 2, SGC_SPMM_NO_HUB = 4,
        SGC_SPMM_HUB_ONLY = 8, SGC_SPMM_ACCUMULATE = 16, SGC_SPMM_HUB_SERIAL = 32,
-       SGC_SPMM_LIGHT_ORDER = 64 };
+       SGC_SPMM_LIGHT_ORDER = 64, SGC_SPMM_X_UNDER_4G = 128 };
 int sgc_spmm_csr_f32_ex(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                         int64_t row_begin, int64_t row_end,
                         const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,

@@ -162,7 +162,7 @@ __device__ __forceinline__ void row_chunks_pipe(const int *__restrict__ col,
 // its last nonzero (never out of bounds) and their FMAs are skipped.
 constexpr int kPairsU = 4;  // nonzero pairs per step (8 nonzeros; 16 in flight)
 
-template <int U>
+template <int U, bool O32>
 __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
                                                const float *__restrict__ val, int k0, int k1,
                                                const float *__restrict__ X, int64_t ldx,
@@ -206,7 +206,11 @@ __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
                 v0[buf][u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(valr), la));
                 v1[buf][u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(valr), lb));
                 const int cj = hi ? cb : ca;
-                xv[buf][u] = *reinterpret_cast<const f4 *>(Xb + (int64_t)cj * row_bytes + boff);
+                if constexpr (O32)
+                    xv[buf][u] = *reinterpret_cast<const f4 *>(
+                        Xb + ((uint32_t)cj * (uint32_t)row_bytes + boff));
+                else
+                    xv[buf][u] = *reinterpret_cast<const f4 *>(Xb + (int64_t)cj * row_bytes + boff);
             }
         };
         issue(k0, 0, colA, valA, 0);
@@ -292,9 +296,9 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
         if constexpr (V == 4 && VH == 2) {
             if (heavy_pairs) {  // the same 128-float sub-chunk, two nonzeros per load
                 const int f = sub * 128 + (lane & 31) * 4;
-                row_pairs_pipe<kPairsU>(col, val, k0, k1, X, ldx,
-                                        Y + (int64_t)(row - row_begin) * ldy, F, f, f < F, true,
-                                        lane, accum != 0);
+                row_pairs_pipe<kPairsU, false>(col, val, k0, k1, X, ldx,
+                                               Y + (int64_t)(row - row_begin) * ldy, F, f, f < F,
+                                               true, lane, accum != 0);
                 return;
             }
         }
@@ -340,7 +344,7 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 // slower on a 76-float slice, profiles/r02/packed_sweep.log).
 constexpr int kRowsU = 4;  // nonzeros per row per step (one b128 (col, val) read each)
 
-template <int LB, int VH, int UH>
+template <int LB, int VH, int UH, bool O32>
 __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
@@ -367,8 +371,9 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
         if (heavy_pairs) {  // n_sub == 1: one item per (row, slice), two nonzeros per load
             const int j = lane & 31;
             const int f = slice * (LR * V) + j * V;
-            row_pairs_pipe<kPairsU>(col, val, k0, k1, X, ldx, Y + (int64_t)(row - row_begin) * ldy,
-                                    F, f, j < LR && f < F_load, vec_store != 0, lane, accum != 0);
+            row_pairs_pipe<kPairsU, O32>(col, val, k0, k1, X, ldx,
+                                         Y + (int64_t)(row - row_begin) * ldy, F, f,
+                                         j < LR && f < F_load, vec_store != 0, lane, accum != 0);
             return;
         }
         const int sub = slice * n_sub + (wave - h * n_sub);  // in units of 64*VH floats
@@ -403,8 +408,14 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
             len = mine ? d : 0;
         }
     }
-    int n_max = 0;
-    for (int s = 0; s < R; ++s) n_max = max(n_max, __builtin_amdgcn_readlane(len, s * LR));
+    // the wave runs to its longest row; up to its shortest every step is
+    // unpredicated (rows in length order make the two close)
+    int n_max = 0, n_min = INT32_MAX;
+    for (int s = 0; s < R; ++s) {
+        const int ls = __builtin_amdgcn_readlane(len, s * LR);
+        n_max = max(n_max, ls);
+        n_min = min(n_min, ls);
+    }
     const int f = slice * (LR * V) + l * V;
     const bool ok = sub < R && f < F_load;
     const uint32_t boff = ok ? uint32_t(f) * 4u : 0u;
@@ -469,8 +480,12 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     vv[slot][4 * q + u] = vq[u];
-                    xv[slot][4 * q + u] =
-                        *reinterpret_cast<const f4 *>(Xb + (int64_t)cc[u] * row_bytes + boff);
+                    if constexpr (O32)  // X spans < 4 GiB: 32-bit row offsets (saddr loads)
+                        xv[slot][4 * q + u] = *reinterpret_cast<const f4 *>(
+                            Xb + ((uint32_t)cc[u] * (uint32_t)row_bytes + boff));
+                    else
+                        xv[slot][4 * q + u] =
+                            *reinterpret_cast<const f4 *>(Xb + (int64_t)cc[u] * row_bytes + boff);
                 }
             }
         };
@@ -487,12 +502,20 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
                     stage(buf ^ 1, colB, valB);
                     issue(buf ^ 1, 0, 0);
                 }
+                if (cur + U <= n_min) {  // every row of the wave has these U (uniform)
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (cur + u < len) {
+                    for (int u = 0; u < U; ++u)
 #pragma unroll
                         for (int v = 0; v < V; ++v)
                             acc[v] = __builtin_fmaf(vv[i & 1][u], xv[i & 1][u][v], acc[v]);
+                } else {  // a row ends inside this step: per-lane predication
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        if (cur + u < len) {
+#pragma unroll
+                            for (int v = 0; v < V; ++v)
+                                acc[v] = __builtin_fmaf(vv[i & 1][u], xv[i & 1][u][v], acc[v]);
+                        }
                     }
                 }
             }
@@ -1012,7 +1035,7 @@ static int g_max_vec = 4;
 // profiles/r02/sweep_rows*.  Set through sgc_set_tuning("rows_per_wave").
 static int g_rows_per_wave = 0;
 
-template <int LB, int VH>
+template <int LB, int VH, bool O32>
 hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int R = kWave / LR, SW = LR * 4;
     const int slices = (F_load + SW - 1) / SW;
@@ -1027,7 +1050,7 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int64_t waves = heavy_waves + (n_light_items + R - 1) / R;
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     dim3 grid((unsigned)blocks, (unsigned)slices);
-    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU>), grid, dim3(kBlock), 0, a.stream,
+    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU, O32>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
                        n_light_items, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
                        a.heavy_threshold, a.accum, a.light_rows, g_heavy_pairs & 1);
@@ -1278,12 +1301,16 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             SGC_HIP_CHECK(hipEventRecord(tl.l0, light_stream));
             tl.kernel = 1;
         }
+        // 32-bit row offsets when the caller vouches that X spans < 4 GiB
+        const bool o32 = (flags & SGC_SPMM_X_UNDER_4G) && ldx * 4 < (int64_t(1) << 32);
+#define SGC_ROWS(LBV, VHV)                                                     \
+    (o32 ? launch_rows<LBV, VHV, true>(a, (int)F4, LR, vec_store)              \
+         : launch_rows<LBV, VHV, false>(a, (int)F4, LR, vec_store))
         if (LR >= 16)
-            e = vh2 ? launch_rows<16, 2>(a, (int)F4, LR, vec_store)
-                    : launch_rows<16, 1>(a, (int)F4, LR, vec_store);
+            e = vh2 ? SGC_ROWS(16, 2) : SGC_ROWS(16, 1);
         else
-            e = vh2 ? launch_rows<8, 2>(a, (int)F4, LR, vec_store)
-                    : launch_rows<8, 1>(a, (int)F4, LR, vec_store);
+            e = vh2 ? SGC_ROWS(8, 2) : SGC_ROWS(8, 1);
+#undef SGC_ROWS
     } else {
         const int V = pick_vec(F_csr, ldx, ldy, X, Y);
         a.F = (int)(V == 4 ? F_csr : F);  // pad columns only with 16-B lanes

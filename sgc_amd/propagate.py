@@ -80,6 +80,13 @@ SPMM_HUB_ONLY = 8  # split launch: only the hub rows, on the current stream
 SPMM_ACCUMULATE = 16  # column-block pass: continue the chains stored in out
 SPMM_HUB_SERIAL = 32  # hub kernel before the light kernel on the same stream
 SPMM_LIGHT_ORDER = 64  # plan rows = heavy rows + the light rows in processing order
+SPMM_X_UNDER_4G = 128  # X spans < 4 GiB: the gathers may use 32-bit row offsets
+
+
+def x_flags(X):
+    """SPMM_X_UNDER_4G when every row of X lies within 4 GiB of its first
+    element (X.shape[0] is the CSR's column count, checked by the callers)."""
+    return SPMM_X_UNDER_4G if X.shape[0] * X.stride(0) * 4 < (1 << 32) else 0
 # Light rows of the multi-row kernel in length order (longest first), so the
 # rows sharing a wavefront have about the same length: a wave runs to its
 # longest row and the other rows' lanes re-load their last nonzero meanwhile
@@ -411,7 +418,7 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
                                            _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
                                            X.stride(0), _lib.ptr(out), out.stride(0), F,
                                            _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
-                                           int(flags) | pl.hub_flags(),
+                                           int(flags) | pl.hub_flags() | x_flags(X),
                                            _lib.stream_handle(X.device)),
                    "spmm_csr_f32")
     return out
@@ -443,7 +450,7 @@ class SpmmLaunch:
         self._args = (_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val),
                       int(row_begin), int(row_end), _lib.ptr(X), X.stride(0), _lib.ptr(out),
                       out.stride(0), F, _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
-                      int(flags) | pl.hub_flags())
+                      int(flags) | pl.hub_flags() | x_flags(X))
 
     def __call__(self, stream_handle):
         rc = self._fn(*self._args, stream_handle)
@@ -527,7 +534,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
             dst = out if h == K - 1 else bufs[nxt][:, :F]
             # the engine's own buffers may be read / written in their pad columns
             flags = ((SPMM_X_PADDED if src is not X else 0) |
-                     (SPMM_Y_PADDED if dst is not out else 0) | pl.hub_flags())
+                     (SPMM_Y_PADDED if dst is not out else 0) | pl.hub_flags() | x_flags(src))
             if hop_hook:
                 hop_hook("start", h)
             _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
