@@ -200,7 +200,7 @@ int sgc_spmm_csr_f32_ex(const int32_t *row_ptr, const int32_t *col_idx, const fl
                         int64_t n_hub, int32_t heavy_threshold, uint32_t flags, void *stream) {
     constexpr uint32_t known = SGC_SPMM_X_PADDED | SGC_SPMM_Y_PADDED | SGC_SPMM_NO_HUB |
                                SGC_SPMM_HUB_ONLY | SGC_SPMM_ACCUMULATE | SGC_SPMM_HUB_SERIAL |
-                               SGC_SPMM_LIGHT_ORDER;
+                               SGC_SPMM_LIGHT_ORDER | SGC_SPMM_X_UNDER_4G;
     SGC_REQUIRE((flags & ~known) == 0, SGC_EINVAL, "spmm_ex: unknown flags 0x%x", flags);
     SGC_REQUIRE(!((flags & SGC_SPMM_NO_HUB) && (flags & SGC_SPMM_HUB_ONLY)), SGC_EINVAL,
                 "spmm_ex: NO_HUB and HUB_ONLY together");

@@ -55,3 +55,18 @@ def test_library_is_gfx950_code_object(lib):
     from sgc_amd import _lib
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_spmm_ex_accepts_every_declared_flag():
+    """Every SGC_SPMM_* bit the header declares passes the flag check (the
+    call then stops at its null pointers, before touching a device)."""
+    import re
+    from sgc_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "sgc_amd.h")).read()
+    bits = [int(v) for v in re.findall(r"SGC_SPMM_\w+ = (\d+)", hdr)]
+    assert 128 in bits
+    lib = _lib.load()
+    for b in bits:
+        rc = lib.sgc_spmm_csr_f32_ex(None, None, None, 0, 0, None, 1, None, 1, 1, None, 0, 0, 0,
+                                     b, None)
+        assert rc != 0 and b"unknown flags" not in lib.sgc_last_error(), b
