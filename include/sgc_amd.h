@@ -242,9 +242,10 @@ int sgc_timing_collect_ex(float *light_ms_host, float *hub_ms_host, float *span_
  * layer sorts them by length, so the rows sharing a wavefront in the
  * multi-row kernel have about the same length and few lanes idle-load past
  * their row's end).  A schedule only: results never depend on it.
- * SGC_SPMM_X_UNDER_4G: the caller vouches that every X row a column id can
- * name lies within 4 GiB of X (n_cols * ldx * 4 < 2^32), so the gathers may
- * use 32-bit row offsets (fewer address instructions per nonzero).  */
+ * SGC_SPMM_X_UNDER_4G: the caller vouches that X has fewer than 2^24 rows
+ * and that every X row a column id can name lies within 4 GiB of X
+ * (n_cols * ldx * 4 < 2^32), so the gathers may use 32-bit row offsets from
+ * one 24-bit multiply (fewer address instructions per nonzero).  */
 enum { SGC_SPMM_X_PADDED = 1, SGC_SPMM_Y_PADDED = 2, SGC_SPMM_NO_HUB = 4,
        SGC_SPMM_HUB_ONLY = 8, SGC_SPMM_ACCUMULATE = 16, SGC_SPMM_HUB_SERIAL = 32,
        SGC_SPMM_LIGHT_ORDER = 64, SGC_SPMM_X_UNDER_4G = 128 };

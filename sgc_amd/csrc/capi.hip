@@ -264,7 +264,8 @@ int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const floa
         const int64_t ldd = last ? ldo : ldw;
         // the workspace buffers' pad columns [F, ldw) may be read and written
         const uint32_t fl = (src != X0 ? SGC_SPMM_X_PADDED : 0u) | (last ? 0u : SGC_SPMM_Y_PADDED) |
-                            (n_rows * lds * 4 < (int64_t(1) << 32) ? SGC_SPMM_X_UNDER_4G : 0u);
+                            (n_rows < (int64_t(1) << 24) && n_rows * lds * 4 < (int64_t(1) << 32)
+                                 ? SGC_SPMM_X_UNDER_4G : 0u);
         const int rc = launch_spmm(row_ptr, col_idx, val, 0, n_rows, src, lds, dst, ldd, F, plan,
                                    plan ? n_heavy : 0, plan ? n_hub : 0, heavy_threshold, fl, s);
         if (rc) return rc;

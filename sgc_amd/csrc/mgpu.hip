@@ -364,7 +364,8 @@ int mgpu_propagate(int64_t handle, const float *X, int64_t ldx, float *Y, int64_
                 // columns; the caller's Y never (its next block lives there)
                 const uint32_t flags =
                     SGC_SPMM_X_PADDED | (last ? 0u : (uint32_t)SGC_SPMM_Y_PADDED) | pl->flags |
-                    (g.n * ld * 4 < (int64_t(1) << 32) ? (uint32_t)SGC_SPMM_X_UNDER_4G : 0u);
+                    (g.n < (int64_t(1) << 24) && g.n * ld * 4 < (int64_t(1) << 32)
+                         ? (uint32_t)SGC_SPMM_X_UNDER_4G : 0u);
                 rc = launch_spmm(r.row_ptr, r.col, r.val, 0, g.n, src, ld, dst, ldd, w, pl->rows,
                                  pl->n_heavy, pl->n_hub, pl->threshold, flags, s.stream);
                 if (rc != SGC_OK) return rc;

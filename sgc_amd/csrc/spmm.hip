@@ -208,7 +208,7 @@ __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
                 const int cj = hi ? cb : ca;
                 if constexpr (O32)
                     xv[buf][u] = *reinterpret_cast<const f4 *>(
-                        Xb + ((uint32_t)cj * (uint32_t)row_bytes + boff));
+                        Xb + (__umul24((uint32_t)cj, (uint32_t)row_bytes) + boff));
                 else
                     xv[buf][u] = *reinterpret_cast<const f4 *>(Xb + (int64_t)cj * row_bytes + boff);
             }
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
                     vv[slot][4 * q + u] = vq[u];
                     if constexpr (O32)  // X spans < 4 GiB: 32-bit row offsets (saddr loads)
                         xv[slot][4 * q + u] = *reinterpret_cast<const f4 *>(
-                            Xb + ((uint32_t)cc[u] * (uint32_t)row_bytes + boff));
+                            Xb + (__umul24((uint32_t)cc[u], (uint32_t)row_bytes) + boff));
                     else
                         xv[slot][4 * q + u] =
                             *reinterpret_cast<const f4 *>(Xb + (int64_t)cc[u] * row_bytes + boff);
@@ -1301,8 +1301,9 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             SGC_HIP_CHECK(hipEventRecord(tl.l0, light_stream));
             tl.kernel = 1;
         }
-        // 32-bit row offsets when the caller vouches that X spans < 4 GiB
-        const bool o32 = (flags & SGC_SPMM_X_UNDER_4G) && ldx * 4 < (int64_t(1) << 32);
+        // 32-bit row offsets (one full-rate 24-bit multiply per gathered row)
+        // when the caller vouches that X spans < 4 GiB and has < 2^24 rows
+        const bool o32 = (flags & SGC_SPMM_X_UNDER_4G) && ldx * 4 < (int64_t(1) << 24);
 #define SGC_ROWS(LBV, VHV)                                                     \
     (o32 ? launch_rows<LBV, VHV, true>(a, (int)F4, LR, vec_store)              \
          : launch_rows<LBV, VHV, false>(a, (int)F4, LR, vec_store))

@@ -84,9 +84,11 @@ SPMM_X_UNDER_4G = 128  # X spans < 4 GiB: the gathers may use 32-bit row offsets
 
 
 def x_flags(X):
-    """SPMM_X_UNDER_4G when every row of X lies within 4 GiB of its first
-    element (X.shape[0] is the CSR's column count, checked by the callers)."""
-    return SPMM_X_UNDER_4G if X.shape[0] * X.stride(0) * 4 < (1 << 32) else 0
+    """SPMM_X_UNDER_4G when X has < 2^24 rows and every row lies within 4 GiB
+    of its first element (X.shape[0] is the CSR's column count, checked by
+    the callers)."""
+    n, ld = X.shape[0], X.stride(0)
+    return SPMM_X_UNDER_4G if n < (1 << 24) and n * ld * 4 < (1 << 32) else 0
 # Light rows of the multi-row kernel in length order (longest first), so the
 # rows sharing a wavefront have about the same length: a wave runs to its
 # longest row and the other rows' lanes re-load their last nonzero meanwhile
