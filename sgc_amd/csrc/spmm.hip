@@ -148,7 +148,7 @@ __device__ __forceinline__ void row_chunks_pipe(const int *__restrict__ col,
         if (ok[c]) *reinterpret_cast<VT *>(Yb + boff[c]) = acc[c];
 }
 
-// row_chunks_pipe scheduled like row_pairs_pipe2: whole 64-nonzero blocks
+// row_chunks_pipe scheduled like row_pairs_pipe: whole 64-nonzero blocks
 // without an exit inside them (the compiler then keeps two steps of gathers
 // in flight instead of draining to zero between steps), the last block stops
 // at the row's end, the (col, val) block after next is loaded before the
@@ -264,6 +264,12 @@ __device__ __forceinline__ void row_chunks_pipe2(const int *__restrict__ col,
 // its last nonzero (never out of bounds) and their FMAs are skipped.
 constexpr int kPairsU = 4;  // nonzero pairs per step (8 nonzeros; 16 in flight)
 
+// Schedule: every 64-nonzero block but the last runs all its steps (no exit
+// inside a block, so the compiler's wait counts keep two steps in flight
+// instead of draining the loads at every block -- with per-step exits they
+// did), the last block stops at the row's end; the (col, val) block after
+// next is loaded before the gathers of the step that starts the next block.
+// Reddit shape K=2: 9.01 -> 8.94 ms, bit-identical (profiles/r03/s5/pairs.log).
 template <int U, bool O32>
 __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
                                                const float *__restrict__ val, int k0, int k1,
@@ -271,113 +277,6 @@ __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
                                                float *__restrict__ yrow, int F, int f_lane,
                                                bool lane_ok, bool vec_store, int lane,
                                                bool accum) {
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    constexpr int kPairs = kWave / (2 * U);  // steps per 64-nonzero block
-    static_assert(kWave % (2 * U) == 0 && kPairs % 2 == 0, "2U must divide 64 into an even count");
-    if (accum && k1 == k0) return;  // nothing to add: the row keeps its partial chains
-    const bool hi = lane >= 32;
-    const uint32_t boff = lane_ok ? uint32_t(f_lane) * 4u : 0u;
-    f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (accum && lane_ok) {  // continue the chains an earlier column-block pass stored
-        if (vec_store) {
-            acc = *reinterpret_cast<const f4 *>(yrow + f_lane);
-        } else {
-#pragma unroll
-            for (int v = 0; v < 4; ++v)
-                if (f_lane + v < F) acc[v] = yrow[f_lane + v];
-        }
-    }
-    if (k1 > k0) {
-        const char *Xb = reinterpret_cast<const char *>(X);
-        const int64_t row_bytes = ldx * 4;
-        const int last = k1 - 1;
-        int colA = ld_meta(col + min(k0 + lane, last));
-        float valA = ld_meta(val + min(k0 + lane, last));
-        int colB = ld_meta(col + min(k0 + kWave + lane, last));
-        float valB = ld_meta(val + min(k0 + kWave + lane, last));
-        f4 xv[2][U];
-        float v0[2][U], v1[2][U];
-        auto issue = [&](int base, int i, int colr, float valr, int buf) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int ka = min(base + i * 2 * U + 2 * u, last);
-                const int kb = min(ka + 1, last);
-                const int la = (ka - base) & (kWave - 1), lb = (kb - base) & (kWave - 1);
-                const int ca = __builtin_amdgcn_readlane(colr, la);
-                const int cb = __builtin_amdgcn_readlane(colr, lb);
-                v0[buf][u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(valr), la));
-                v1[buf][u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(valr), lb));
-                const int cj = hi ? cb : ca;
-                if constexpr (O32)
-                    xv[buf][u] = *reinterpret_cast<const f4 *>(
-                        Xb + (__umul24((uint32_t)cj, (uint32_t)row_bytes) + boff));
-                else
-                    xv[buf][u] = *reinterpret_cast<const f4 *>(Xb + (int64_t)cj * row_bytes + boff);
-            }
-        };
-        issue(k0, 0, colA, valA, 0);
-        for (int base = k0;; base += kWave) {
-#pragma unroll
-            for (int i = 0; i < kPairs; ++i) {
-                const int cur = base + i * 2 * U;
-                if (cur > last) break;  // uniform; the step issued for it is dropped
-                if (i + 1 < kPairs)
-                    issue(base, i + 1, colA, valA, (i + 1) & 1);
-                else  // first step of the next block, from its prefetched (col, val)
-                    issue(base + kWave, 0, colB, valB, 0);
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int ka = cur + 2 * u;
-                    if (ka > last) break;  // uniform
-                    f4 xa, xb;
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        const uint32_t x = __float_as_uint(xv[i & 1][u][v]);
-                        // [x.lo | x.hi] -> lanes all x_k (lo), all x_k+1 (hi)
-                        const auto t = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-                        xa[v] = __uint_as_float(t[0]);
-                        xb[v] = __uint_as_float(t[1]);
-                    }
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) acc[v] = __builtin_fmaf(v0[i & 1][u], xa[v], acc[v]);
-                    if (ka + 1 <= last) {
-#pragma unroll
-                        for (int v = 0; v < 4; ++v)
-                            acc[v] = __builtin_fmaf(v1[i & 1][u], xb[v], acc[v]);
-                    }
-                }
-            }
-            if (base + kWave > last) break;
-            colA = colB;
-            valA = valB;
-            colB = ld_meta(col + min(base + 2 * kWave + lane, last));
-            valB = ld_meta(val + min(base + 2 * kWave + lane, last));
-        }
-    }
-    if (!hi && lane_ok) {
-        if (vec_store) {
-            *reinterpret_cast<f4 *>(yrow + f_lane) = acc;
-        } else {
-#pragma unroll
-            for (int v = 0; v < 4; ++v)
-                if (f_lane + v < F) yrow[f_lane + v] = acc[v];
-        }
-    }
-}
-
-// row_pairs_pipe with the schedule of the multi-row kernel's P2 light loop:
-// every 64-nonzero block but the last runs all its steps (no exit inside a
-// block, so the compiler's wait counts keep two steps in flight instead of
-// draining to zero at every block), the last block stops at the row's end;
-// the (col, val) block after next is loaded before the gathers of the step
-// that starts the next block.  Same loads, same FMA order.
-template <int U, bool O32>
-__device__ __forceinline__ void row_pairs_pipe2(const int *__restrict__ col,
-                                                const float *__restrict__ val, int k0, int k1,
-                                                const float *__restrict__ X, int64_t ldx,
-                                                float *__restrict__ yrow, int F, int f_lane,
-                                                bool lane_ok, bool vec_store, int lane,
-                                                bool accum) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     constexpr int kPairs = kWave / (2 * U);  // steps per 64-nonzero block
     static_assert(kWave % (2 * U) == 0 && kPairs % 2 == 0, "2U must divide 64 into an even count");
@@ -569,7 +468,7 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 // slower on a 76-float slice, profiles/r02/packed_sweep.log).
 constexpr int kRowsU = 4;  // nonzeros per row per step (one b128 (col, val) read each)
 
-template <int LB, int VH, int UH, bool O32, bool P2>
+template <int LB, int VH, int UH, bool O32>
 __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
@@ -581,9 +480,8 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     static_assert(kSteps >= 2 && kSteps % 2 == 0, "bad block");
     typedef float f4 __attribute__((ext_vector_type(4)));
     typedef int i4 __attribute__((ext_vector_type(4)));
-    // (P2: LB more slots per buffer, the write target of lanes that stage nothing)
-    __shared__ __attribute__((aligned(16))) int s_col[kBlock / kWave][2][kWave + (P2 ? LB : 0)];
-    __shared__ __attribute__((aligned(16))) float s_val[kBlock / kWave][2][kWave + (P2 ? LB : 0)];
+    __shared__ __attribute__((aligned(16))) int s_col[kBlock / kWave][2][kWave];
+    __shared__ __attribute__((aligned(16))) float s_val[kBlock / kWave][2][kWave];
     const int lane = threadIdx.x & (kWave - 1);
     const int wl = threadIdx.x / kWave;
     const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kBlock / kWave) + wl));
@@ -597,16 +495,9 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
         if (heavy_pairs & 1) {  // n_sub == 1: one item per (row, slice), two nonzeros per load
             const int j = lane & 31;
             const int f = slice * (LR * V) + j * V;
-            if (heavy_pairs & 2)
-                row_pairs_pipe2<kPairsU, O32>(col, val, k0, k1, X, ldx,
-                                              Y + (int64_t)(row - row_begin) * ldy, F, f,
-                                              j < LR && f < F_load, vec_store != 0, lane,
-                                              accum != 0);
-            else
-                row_pairs_pipe<kPairsU, O32>(col, val, k0, k1, X, ldx,
-                                             Y + (int64_t)(row - row_begin) * ldy, F, f,
-                                             j < LR && f < F_load, vec_store != 0, lane,
-                                             accum != 0);
+            row_pairs_pipe<kPairsU, O32>(col, val, k0, k1, X, ldx,
+                                         Y + (int64_t)(row - row_begin) * ldy, F, f,
+                                         j < LR && f < F_load, vec_store != 0, lane, accum != 0);
             return;
         }
         const int sub = slice * n_sub + (wave - h * n_sub);  // in units of 64*VH floats
@@ -667,102 +558,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
                 if (f + v < F) acc[v] = yr[f + v];
         }
     }
-    if (P2 && n_max > 0) {
-        // Same FMA chains, scheduled so that the compiler's wait counts keep
-        // two steps of gathers in flight: whole LDS blocks run every step (no
-        // exit inside a block), only the last block stops at the wave's
-        // longest row; (col, val) loads and LDS writes are unconditional
-        // (every lane loads a valid index, lanes that stage nothing write a
-        // spare LDS slot), and the block after next is fetched before the
-        // gathers of the step that stages the next one.  (The per-step exits
-        // of the form below made the compiler drain the loads to one or zero
-        // in flight before most steps.)
-        const char *Xb = reinterpret_cast<const char *>(X);
-        const int64_t row_bytes = ldx * 4;
-        const bool stager = sub < R && l < LB;
-        const int wslot = stager ? lds_row + l : kWave + (lane & (LB - 1));
-        // nonzero base + l of this lane's row, clamped to its last one; a row
-        // without nonzeros reads index 0 (valid: n_max > 0) and skips its FMAs
-        auto fidx = [&](int base) { return len > 0 ? k0 + min(base + l, len - 1) : 0; };
-        auto stage = [&](int buf, int c, float v) {
-            s_col[wl][buf][wslot] = c;
-            s_val[wl][buf][wslot] = v;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        };
-        {
-            const int i0 = fidx(0);
-            stage(0, col[i0], val[i0]);
-        }
-        int iB = fidx(LB);
-        int colB = col[iB];
-        float valB = val[iB];
-        f4 xv[2][U];
-        float vv[2][U];
-        auto issue = [&](int buf, int i, int slot) {
-#pragma unroll
-            for (int q = 0; q < U / 4; ++q) {
-                const i4 cc =
-                    *reinterpret_cast<const i4 *>(&s_col[wl][buf][lds_row + i * U + 4 * q]);
-                const f4 vq =
-                    *reinterpret_cast<const f4 *>(&s_val[wl][buf][lds_row + i * U + 4 * q]);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    vv[slot][4 * q + u] = vq[u];
-                    if constexpr (O32)
-                        xv[slot][4 * q + u] = *reinterpret_cast<const f4 *>(
-                            Xb + (__umul24((uint32_t)cc[u], (uint32_t)row_bytes) + boff));
-                    else
-                        xv[slot][4 * q + u] =
-                            *reinterpret_cast<const f4 *>(Xb + (int64_t)cc[u] * row_bytes + boff);
-                }
-            }
-        };
-        // one step: issue the gathers of step i + 1 (after the last step of
-        // a block: stage the next block, fetch the one after it, issue its
-        // first step), then the FMAs of step i
-        auto step = [&](int base, int buf, int i, bool last_block) {
-            const int cur = base + i * U;
-            if (i + 1 < kSteps) {
-                issue(buf, i + 1, (i + 1) & 1);
-            } else if (!last_block) {
-                stage(buf ^ 1, colB, valB);
-                if (base + 2 * LB < n_max) {
-                    iB = fidx(base + 2 * LB);
-                    colB = col[iB];
-                    valB = val[iB];
-                }
-                issue(buf ^ 1, 0, 0);
-            }
-            if (cur + U <= n_min) {  // every row of the wave has these U (uniform)
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-#pragma unroll
-                    for (int v = 0; v < V; ++v)
-                        acc[v] = __builtin_fmaf(vv[i & 1][u], xv[i & 1][u][v], acc[v]);
-            } else {  // a row ends inside this step: per-lane predication
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (cur + u < len) {
-#pragma unroll
-                        for (int v = 0; v < V; ++v)
-                            acc[v] = __builtin_fmaf(vv[i & 1][u], xv[i & 1][u][v], acc[v]);
-                    }
-                }
-            }
-        };
-        issue(0, 0, 0);
-        const int nb = (n_max + LB - 1) / LB;  // LDS blocks (wave-uniform)
-        int base = 0;
-        for (int b = 0; b + 1 < nb; ++b, base += LB) {
-#pragma unroll
-            for (int i = 0; i < kSteps; ++i) step(base, b & 1, i, false);
-        }
-#pragma unroll
-        for (int i = 0; i < kSteps; ++i)  // no exit: skipped steps fall through
-            if (base + i * U < n_max) step(base, (nb - 1) & 1, i, true);
-    } else if (!P2 && n_max > 0) {
+    if (n_max > 0) {
         const char *Xb = reinterpret_cast<const char *>(X);
         const int64_t row_bytes = ldx * 4;
         // lanes l < LB stage (col, val) of their row's nonzero base + l,
@@ -1325,9 +1121,12 @@ constexpr int kHeavyU = 16;
 // the multi-row kernel (Reddit shape K=2: 9.29 -> 9.12 ms, profiles/r03/s1/ab.log),
 // bit 1 = in the one-row kernel.  Set through sgc_set_tuning("heavy_pairs").
 static int g_heavy_pairs = 1;
-// One-row kernel (light rows and heavy sub-chunks): 1 = row_chunks_pipe2,
-// 0 = row_chunks_pipe.  Set through sgc_set_tuning("chunks_pipe").
-static int g_chunks_pipe = 0;
+// One-row kernel: row_chunks_pipe2 (whole-block schedule) on launches of at
+// least this many rows, row_chunks_pipe below.  Measured bit-identical,
+// interleaved (profiles/r03/s5/chunks_*.log): RMAT shape K=3 (4.2 M rows)
+// 95.5 -> 94.1 ms; Pubmed shape K=2 (19.7 k rows, latency-bound) 0.102 ->
+// 0.109 ms.
+constexpr int kChunksPipe2Rows = 1 << 20;
 
 template <int V, int C>
 hipError_t launch_vc(const LaunchArgs &a) {
@@ -1341,7 +1140,7 @@ hipError_t launch_vc(const LaunchArgs &a) {
     hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin, a.n_rows,
                        a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold, a.accum,
-                       ((g_heavy_pairs >> 1) & 1) | (g_chunks_pipe << 1));
+                       ((g_heavy_pairs >> 1) & 1) | (a.n_rows >= kChunksPipe2Rows ? 2 : 0));
     return hipGetLastError();
 }
 
@@ -1366,15 +1165,7 @@ static int g_max_vec = 4;
 // profiles/r02/sweep_rows*.  Set through sgc_set_tuning("rows_per_wave").
 static int g_rows_per_wave = 0;
 
-// Light rows of the multi-row kernel: 1 = the schedule that keeps two steps
-// of gathers in flight (P2), 0 = the round-2 loop.  Set through
-// sgc_set_tuning("light_pipe").
-static int g_light_pipe = 0;
-// Heavy pairs of the multi-row kernel: 1 = row_pairs_pipe2, 0 = row_pairs_pipe.
-// Set through sgc_set_tuning("pairs_pipe").
-static int g_pairs_pipe = 0;
-
-template <int LB, int VH, bool O32, bool P2>
+template <int LB, int VH, bool O32>
 hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int R = kWave / LR, SW = LR * 4;
     const int slices = (F_load + SW - 1) / SW;
@@ -1389,11 +1180,10 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int64_t waves = heavy_waves + (n_light_items + R - 1) / R;
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     dim3 grid((unsigned)blocks, (unsigned)slices);
-    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU, O32, P2>), grid, dim3(kBlock), 0, a.stream,
+    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU, O32>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
                        n_light_items, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
-                       a.heavy_threshold, a.accum, a.light_rows,
-                       (g_heavy_pairs & 1) | (g_pairs_pipe << 1));
+                       a.heavy_threshold, a.accum, a.light_rows, g_heavy_pairs & 1);
     return hipGetLastError();
 }
 
@@ -1468,21 +1258,6 @@ int set_tuning(const char *key, int64_t value) {
         g_heavy_pairs = (int)value;
         return SGC_OK;
     }
-    if (std::string(key) == "chunks_pipe") {
-        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "chunks_pipe must be 0 or 1");
-        g_chunks_pipe = (int)value;
-        return SGC_OK;
-    }
-    if (std::string(key) == "pairs_pipe") {
-        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "pairs_pipe must be 0 or 1");
-        g_pairs_pipe = (int)value;
-        return SGC_OK;
-    }
-    if (std::string(key) == "light_pipe") {
-        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "light_pipe must be 0 or 1");
-        g_light_pipe = (int)value;
-        return SGC_OK;
-    }
     if (std::string(key) == "max_vec") {
         SGC_REQUIRE(value == 1 || value == 2 || value == 4, SGC_EINVAL, "max_vec must be 1, 2 or 4");
         g_max_vec = (int)value;
@@ -1495,9 +1270,6 @@ int set_tuning(const char *key, int64_t value) {
 int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "slice_floats") return g_slice_floats;
     if (key && std::string(key) == "max_vec") return g_max_vec;
-    if (key && std::string(key) == "light_pipe") return g_light_pipe;
-    if (key && std::string(key) == "pairs_pipe") return g_pairs_pipe;
-    if (key && std::string(key) == "chunks_pipe") return g_chunks_pipe;
     if (key && std::string(key) == "heavy_pairs") return g_heavy_pairs;
     if (key && std::string(key) == "rows_per_wave") return g_rows_per_wave;
     if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
@@ -1662,17 +1434,14 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         // 32-bit row offsets (one full-rate 24-bit multiply per gathered row)
         // when the caller vouches that X spans < 4 GiB and has < 2^24 rows
         const bool o32 = (flags & SGC_SPMM_X_UNDER_4G) && ldx * 4 < (int64_t(1) << 24);
-#define SGC_ROWS2(LBV, VHV, P2V)                                               \
-    (o32 ? launch_rows<LBV, VHV, true, P2V>(a, (int)F4, LR, vec_store)         \
-         : launch_rows<LBV, VHV, false, P2V>(a, (int)F4, LR, vec_store))
-#define SGC_ROWS(LBV, VHV) \
-    (g_light_pipe ? SGC_ROWS2(LBV, VHV, true) : SGC_ROWS2(LBV, VHV, false))
+#define SGC_ROWS(LBV, VHV)                                                     \
+    (o32 ? launch_rows<LBV, VHV, true>(a, (int)F4, LR, vec_store)              \
+         : launch_rows<LBV, VHV, false>(a, (int)F4, LR, vec_store))
         if (LR >= 16)
             e = vh2 ? SGC_ROWS(16, 2) : SGC_ROWS(16, 1);
         else
             e = vh2 ? SGC_ROWS(8, 2) : SGC_ROWS(8, 1);
 #undef SGC_ROWS
-#undef SGC_ROWS2
     } else {
         const int V = pick_vec(F_csr, ldx, ldy, X, Y);
         a.F = (int)(V == 4 ? F_csr : F);  // pad columns only with 16-B lanes
