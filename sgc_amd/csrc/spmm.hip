@@ -1058,6 +1058,7 @@ struct TimedLaunch {
     hipEvent_t l0 = nullptr, l1 = nullptr, h0 = nullptr, h1 = nullptr;
     int kernel = -1;      // light kernel: 0 spmm_csr_kernel, 1 spmm_rows_kernel, -1 none
     bool serial = false;  // hub kernel ran before the light kernel on the same stream
+    bool hub_first = false;  // concurrent: hub kernel on the caller's stream, light on the side
 };
 static std::mutex g_timing_mu;
 static bool g_timing = false;
@@ -1212,12 +1213,19 @@ constexpr int max_chunks(int V) { return 16 / V; }  // <= 16 accumulators per la
 static int g_slice_floats = 128;
 // Hub-kernel feature chunk: 0 = auto (32 on 128-B aligned X rows, else 64).
 static int g_hub_chunk = 0;
-// Where the hub kernel runs: 1 = a side stream, concurrent with the light
-// kernel (fork + join events: ~20-30 us of cross-queue synchronisation per
-// launch); 2 = the caller's stream, before the light kernel (serial: costs
-// the hub kernel's own time); 0 = per launch, serial when the caller sets
-// SGC_SPMM_HUB_SERIAL (the Python layer does when the longest hub chain is
-// shorter than that synchronisation: Pubmed shape 70 -> 61 us per hop).
+// Where the hub kernel runs: 1 = concurrent with the light kernel -- the hub
+// kernel on the caller's stream, the light kernel on a side stream (fork +
+// join events: ~20-30 us of cross-queue synchronisation per launch); 2 = the
+// caller's stream, before the light kernel (serial: costs the hub kernel's
+// own time); 0 = per launch, serial when the caller sets SGC_SPMM_HUB_SERIAL
+// (the Python layer does when the longest hub chain is shorter than that
+// synchronisation: Pubmed shape 70 -> 61 us per hop), else concurrent.
+// Concurrent launches put the HUB kernel on the caller's stream because the
+// stream that waits on the fork event starts a few microseconds later: with
+// the light kernel first, its 256-thread workgroups fill every CU and the
+// 1024-thread hub workgroups trickled in as whole CUs drained, ending up to
+// 0.26 ms after it (profiles/r03/s6 trace); hub first: Reddit K=2 8.96 ->
+// 8.91 ms, one 76-float pass 0.91 -> 0.77 ms (profiles/r03/s7/stream3*.log).
 // Set through sgc_set_tuning("hub_stream").
 static int g_hub_stream = 0;
 // Loader waves per hub workgroup: 15 or 7 (spmm_hub_kernel).  Set through
@@ -1328,15 +1336,15 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     SideJoin side_join;
     hipStream_t light_stream = stream;
     if (n_hub > 0) {
-        // hub rows (the heaviest n_hub of the plan) run on the side stream
-        // 32-feature chunks spread a hub over more CUs; measured faster up to
+        // hub rows (the heaviest n_hub of the plan) run beside the light
+        // kernel (g_hub_stream); 32-feature chunks spread a hub over more CUs; measured faster up to
         // F = 160 and slower from F = 320 (scripts/sweep_narrow.py), and they
         // need 128-B aligned rows to stay one line per segment.
         const bool lines = ldx % 32 == 0 && reinterpret_cast<uintptr_t>(X) % 128 == 0;
         const int hc = g_hub_chunk ? g_hub_chunk : (lines && F <= 192 ? 32 : 64);
         const int n_chunks = (int)((F + hc - 1) / hc);
         SGC_REQUIRE(n_hub * n_chunks < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many hub items");
-        hipStream_t hs = stream;  // HUB_ONLY: on the caller's stream, nothing else
+        const hipStream_t hs = stream;  // always the caller's stream
         const bool serial =
             g_hub_stream == 2 || (g_hub_stream == 0 && (flags & SGC_SPMM_HUB_SERIAL));
         if (!hub_only && !serial) {
@@ -1346,7 +1354,8 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
             side_join.side = side;  // from here on every exit joins
             side_join.stream = stream;
-            hs = side->s;
+            light_stream = side->s;  // the hub kernel stays on the caller's stream
+            tl.hub_first = true;
         }
         if (timing) {
             SGC_HIP_CHECK(pooled_event(&tl.h0));
@@ -1513,9 +1522,9 @@ int timing_collect_ex(float *light_ms, float *hub_ms, float *span_ms, int32_t *k
             float to_end = 0.0f;
             if (t.serial) {  // h0 ... h1 l0 ... l1 on one stream
                 SGC_HIP_CHECK(hipEventElapsedTime(&span, t.h0, t.l1));
-            } else {  // the side stream starts at the fork, just before l0
-                SGC_HIP_CHECK(hipEventElapsedTime(&to_end, t.l0, t.h1));
-                span = std::max(span, to_end);
+            } else if (t.hub_first) {  // h0 on the caller's stream, l0 after the fork
+                SGC_HIP_CHECK(hipEventElapsedTime(&to_end, t.h0, t.l1));
+                span = std::max(hub_ms[i], to_end);
             }
         }
         if (span_ms) span_ms[i] = span;
