@@ -58,7 +58,15 @@ def main():
     ap.add_argument("--align", type=int, default=4)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--bw", default="150,300,450", help="assumed all-to-all ingress GB/s per rank")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="schedule knob for sgc_set_tuning (results never depend on it)")
     args = ap.parse_args()
+    if args.tune:
+        from sgc_amd import _lib
+        for kv in args.tune:
+            k, v = kv.split("=")
+            _lib.check(_lib.load().sgc_set_tuning(k.encode(), int(v)), f"set_tuning {kv}")
+        print(json.dumps({"case": "tuning", "tune": args.tune}), flush=True)
     spec = graphs.SHAPES[args.shape]
     S = graphs.synthetic_graph(args.shape, seed=0)
     F, K, n = spec["features"], spec["hops"], S.n

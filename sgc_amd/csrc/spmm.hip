@@ -1160,11 +1160,21 @@ static int g_max_vec = 4;
 // Light kernel choice when 16-B lanes are possible (F rounded up to 4 fits
 // the rows and they are 16-B aligned): 0 = auto -- spmm_rows_kernel when
 // spmm_csr_kernel could not use 16-B lanes itself (F % 4 != 0: Reddit's 602)
-// or the launch is narrower than 128 floats, else spmm_csr_kernel (F = 256 /
-// 500: its one-row 256-float slices measured faster); 2 / 4 = always
+// or the launch is narrower than 128 floats or a large one at 128 / > 256
+// floats (kWideRowsMin below), else spmm_csr_kernel (F = 152 .. 256, and
+// Pubmed's 500: its one-row 256-float slices measured faster); 2 / 4 = always
 // spmm_rows_kernel with 32 / 16 lanes per row on wide launches; 1 = never.
 // profiles/r02/sweep_rows*.  Set through sgc_set_tuning("rows_per_wave").
 static int g_rows_per_wave = 0;
+// Large launches with 16-B lanes at F4 == 128 or F4 > 256 take the
+// multi-row kernel (128-float slices, two rows per wave) even when
+// spmm_csr_kernel could use 16-B lanes: one hop over the Reddit-shape graph
+// (interleaved, bit-identical, profiles/r03/s10/ab_reddit.log) at 304 floats
+// (the P = 2 feature block) 3.00 -> 2.50 ms, at 128 1.00 -> 0.94; at 152 / 160
+// the one-row kernel's single 256-float slice stays faster (1.46 vs 1.60), and
+// at 256 it is the RMAT shape's kernel (31.6 vs 37.3 ms per hop).  Small
+// launches (Pubmed shape, F = 500) stay latency-bound on the one-row kernel.
+constexpr int64_t kWideRowsMin = 65536;
 
 template <int LB, int VH, bool O32>
 hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
@@ -1418,8 +1428,9 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     // the default schedule knobs.
     const bool small_wide = n_rows * F <= (int64_t(1) << 23) && F > 256 &&
                             g_rows_per_wave == 0 && g_slice_floats == 128;
+    const bool wide_rows = n_rows >= kWideRowsMin && (F4 == 128 || F4 > 256);
     const bool rows_kernel = v4_ok && g_rows_per_wave != 1 && !small_wide &&
-                             (g_rows_per_wave > 1 || !csr_v4 || F4 < 128);
+                             (g_rows_per_wave > 1 || !csr_v4 || F4 < 128 || wide_rows);
     hipError_t e = hipSuccess;
     if (rows_kernel) {
         const int vec_store = ldy % 4 == 0 && ya % 16 == 0 && F4 <= ldy &&

@@ -74,6 +74,32 @@ def test_heavy_split_schedule_never_changes_bits(tiny_cases, threshold, hub, hub
         lib.sgc_set_tuning(b"rows_per_wave", 0)
 
 
+@pytest.mark.parametrize("F", [128, 304, 300, 152])
+def test_wide_launch_kernel_choice_bit_exact(oracle, F):
+    """Launches of >= 65,536 rows: at F = 128 and F > 256 with 16-B lanes the
+    multi-row kernel runs (128-float slices), at 152 the one-row kernel; both
+    in the engine's padded buffers (the feature partition's P = 2 / P = 4
+    blocks) and in a caller's unpadded tensor: the oracle's bits."""
+    from sgc_amd import graphs
+    from sgc_amd.propagate import SPMM_X_PADDED, SPMM_Y_PADDED, DeviceCSR, spmm
+    n = 70000
+    S = graphs.synthetic_graph("pubmed", seed=5, n=n, edges=350000)
+    X = np.random.default_rng(F).standard_normal((n, F)).astype(np.float32)
+    want = oracle.spmm_csr(S.row_ptr, S.col_idx, S.val, X, 0, n)
+    csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=DEV)
+    ld = (F + 31) // 32 * 32
+    Xp = torch.zeros((n, ld), device=DEV)
+    Xp[:, :F] = torch.from_numpy(X)
+    Yp = torch.full((n, ld), float("nan"), device=DEV)
+    for th, hub in ((None, None), (16, 200), (10**9, 10**9)):
+        kw = {} if th is None else {"threshold": th, "hub_threshold": hub}
+        spmm(csr, Xp[:, :F], 0, n, out=Yp[:, :F], flags=SPMM_X_PADDED | SPMM_Y_PADDED, **kw)
+        y = spmm(csr, Xp[:, :F].contiguous(), 0, n, **kw)
+        torch.cuda.synchronize()
+        assert bits_equal(Yp[:, :F].cpu().numpy(), want), (F, th)
+        assert bits_equal(y.cpu().numpy(), want), (F, th)
+
+
 def _schedule_cases(tiny_cases, threshold, hub):
     from sgc_amd.propagate import DeviceCSR, propagate
     for name in ("hub1000_F65", "hub1000_F130", "norm_n48_F602", "norm_n48_F130",
