@@ -386,9 +386,12 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
             spmm_fn=bracket(lambda X, r0, r1, out: spmm_hip(
                 csr, X, r0, r1, out=out, threshold=args.threshold,
                 hub_threshold=args.hub_threshold), launch_bytes),
-            chunks=args.chunks, host_staging=staging)
+            chunks=args.chunks, host_staging=staging, exchange=args.exchange)
         fb, fB = feature_bounds(F, world)
-        exch = ("one all-to-all of the row blocks of X_K" if output == "sharded" else
+        pairwise = args.exchange == "pairwise" or (args.exchange == "auto" and world == 2)
+        exch = ((f"a pairwise exchange of the row blocks of X_K overlapped with the last hop "
+                 f"({prop._pieces(world)} piece(s) per destination)" if pairwise else
+                 "one all-to-all of the row blocks of X_K") if output == "sharded" else
                 f"one all-gather of X_K pipelined with the last hop in {args.chunks} row chunks")
         par = (f"feature-partition x{world} ({fB}-column blocks, all K hops local) + {backend} "
                f"{exch}; output {output}")
@@ -528,6 +531,9 @@ def main():
                     help="N>1 cyclic: rows per round-robin tile")
     ap.add_argument("--col-blocks", type=int, default=2,
                     help="N>1 tiles: feature blocks C (P = R x C)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "pairwise"],
+                    help="feature partition, sharded output: all-to-all after the last hop, or "
+                         "pairwise P2P overlapped with it (auto: pairwise at N = 2)")
     ap.add_argument("--output", default="sharded", choices=["sharded", "replicated"],
                     help="N>1: each rank keeps its row block of X_K, or all ranks get all of it")
     ap.add_argument("--chunks", type=int, default=4,

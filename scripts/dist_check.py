@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--col-blocks", type=int, default=2)
     ap.add_argument("--row-chunks", type=int, default=1)
     ap.add_argument("--group-floats", type=int, default=0)
+    ap.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "pairwise"],
+                    help="features: the sharded exchange")
+    ap.add_argument("--pieces", type=int, default=None, help="features: pairwise row pieces")
     ap.add_argument("--device", default="cuda", help="cpu: the CPU-twin rehearsal")
     ap.add_argument("--cache", default=os.environ.get("TMPDIR", "/tmp"))
     args = ap.parse_args()
@@ -83,7 +86,8 @@ def main():
         from sgc_amd.propagate import DeviceCSR
         csr = DeviceCSR.from_host_arrays(np.asarray(S.row_ptr), np.asarray(S.col_idx),
                                          np.asarray(S.val), device=dev)
-        fp = FeaturePartitionedPropagator(csr, host_staging=True)
+        fp = FeaturePartitionedPropagator(csr, host_staging=True, exchange=args.exchange,
+                                          pieces=args.pieces)
         mine = fp.propagate(X, K, output="sharded")
         rb = equal_row_bounds(g["n"], world)
         r0, r1 = int(rb[rank]), int(rb[rank + 1])

@@ -1,6 +1,7 @@
 """Rehearse the feature partition's per-rank step on ONE GPU.
 
     python scripts/feature_rehearsal.py [--shape reddit] [--P 2,4,8] [--align 4]
+                                        [--exchange alltoall,pairwise] [--link-gbps 57.6]
 
 FeaturePartitionedPropagator needs no exchange between hops (column f of
 X_{k+1} depends on column f of X_k only); its one exchange is the all-to-all
@@ -9,8 +10,11 @@ layout the row partition ends with).  Here each rank's exact step runs
 through the propagator itself with that all-to-all replaced by a local copy
 of the send buffer, so what is timed is the rank's compute (block copy,
 K hops over all rows at the block's width, unpack of the P received blocks).
-The all-to-all is then added at an assumed per-rank ingress bandwidth:
-(P-1)/P of ceil(N/P) x B x 4 bytes per rank.  One JSON line per case.
+The exchange is then modelled at a stated link rate: one xGMI link per GPU
+pair, --link-gbps each way, so a rank's ingress is (P-1) links; the
+all-to-all ((P-1)/P of ceil(N/P) x B x 4 bytes per rank) after the last hop,
+the pairwise exchange overlapped with it on a timeline (pairwise_projection).
+One JSON line per case.
 """
 import argparse
 import json
@@ -23,16 +27,42 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from sgc_amd import graphs  # noqa: E402
-from sgc_amd.distributed import FeaturePartitionedPropagator, feature_bounds  # noqa: E402
-from sgc_amd.propagate import DeviceCSR, propagate  # noqa: E402
+from sgc_amd.distributed import FeaturePartitionedPropagator, _copy_cols, feature_bounds  # noqa: E402
+from sgc_amd.propagate import SPMM_X_PADDED, SPMM_Y_PADDED, DeviceCSR, propagate  # noqa: E402
 
 
 class LocalFeaturePropagator(FeaturePartitionedPropagator):
-    """The feature partition with the all-to-all replaced by a local copy."""
+    """The feature partition with the exchange replaced by local copies."""
 
     def _all_to_all(self, recv, send):
         recv.copy_(send)
         return None
+
+    def _exchange_pair(self, send, dst, recv, src):
+        m = min(send.shape[0], recv.shape[0])
+        if m:
+            recv[:m].copy_(send[:m])
+        return []
+
+
+def pairwise_projection(t_c, t_hop, t_unpack, P, k, piece_bytes, link_gbps):
+    """Step time of the pairwise exchange: hop K starts at t0 = t_c - t_hop -
+    t_unpack and computes the P-1 destination blocks in k pieces each, then
+    the rank's own block (equal time per row); piece i of destination j is
+    sent when computed, on the link to that peer (one link per GPU pair,
+    full duplex: a rank's sends to different peers run in parallel, pieces to
+    one peer in sequence); the unpack waits for the last receive."""
+    t0 = t_c - t_hop - t_unpack
+    dt = t_hop / (P * k)
+    lt = piece_bytes / (link_gbps * 1e9) * 1e3
+    end = 0.0
+    for j in range(P - 1):
+        free = 0.0
+        for i in range(k):
+            ready = t0 + (j * k + i + 1) * dt
+            free = max(free, ready) + lt
+        end = max(end, free)
+    return max(t_c, end + t_unpack)
 
 
 def timeit(fn, reps, warm=3):
@@ -57,7 +87,10 @@ def main():
     ap.add_argument("--P", default="2,4,8")
     ap.add_argument("--align", type=int, default=4)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--bw", default="150,300,450", help="assumed all-to-all ingress GB/s per rank")
+    ap.add_argument("--link-gbps", type=float, default=57.6,
+                    help="per-peer xGMI rate each way (one link per GPU pair): a rank's "
+                         "ingress is (P-1) x this")
+    ap.add_argument("--exchange", default="alltoall,pairwise")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="schedule knob for sgc_set_tuning (results never depend on it)")
     args = ap.parse_args()
@@ -75,40 +108,64 @@ def main():
     out = torch.empty((n, F), device="cuda")
     t1 = timeit(lambda: propagate(csr, X0, K, out=out), args.reps)
     print(json.dumps({"case": "single", "shape": args.shape, "ms": t1}), flush=True)
-    bws = [float(b) for b in args.bw.split(",")]
     for P in (int(p) for p in args.P.split(",")):
         fb, B = feature_bounds(F, P, args.align)
         Bn = -(-n // P)
         a2a = (P - 1) * Bn * B * 4  # bytes a rank receives
-        ranks = []
-        seen = {}
-        for p in range(P):
-            w = int(fb[p + 1] - fb[p])
-            if w in seen:  # same block width, same work
-                ranks.append(seen[w])
-                continue
-            prop = LocalFeaturePropagator(csr, rank=p, world_size=P, align=args.align)
-            t = timeit(lambda: prop.propagate(X0, K, output="sharded"), args.reps)
-            hop = timeit(lambda: prop.spmm_fn(X0[:, int(fb[p]):int(fb[p + 1])], 0, n,
-                                              prop._buf("send", (P * Bn, B), X0)[:n, :w]),
-                         args.reps)
-            rec = {"case": "rank", "P": P, "rank": p, "cols": w, "compute_ms": t,
-                   "one_hop_unaligned_ms": hop}
-            print(json.dumps(rec), flush=True)
-            seen[w] = rec
-            ranks.append(rec)
-            del prop
-            torch.cuda.empty_cache()
-        worst = max(r["compute_ms"] for r in ranks)
-        proj = {f"{bw:g}GBps": worst + a2a / (bw * 1e9) * 1e3 for bw in bws}
-        print(json.dumps({"case": "summary", "P": P, "block_floats": B, "single_ms": t1,
-                          "max_rank_compute_ms": worst, "compute_only_speedup": t1 / worst,
-                          "all_to_all_MB_per_rank": round(a2a / 1e6, 1),
-                          "projected_step_ms": proj,
-                          "projected_speedup": {k: t1 / v for k, v in proj.items()},
-                          "assumption": "all-to-all not overlapped, at the given per-rank "
-                                        "ingress GB/s; compute measured on one GPU per rank"}),
-              flush=True)
+        ingress = (P - 1) * args.link_gbps
+        for mode in args.exchange.split(","):
+            ranks = []
+            seen = {}
+            for p in range(P):
+                w = int(fb[p + 1] - fb[p])
+                if w in seen:  # same block width, same work
+                    ranks.append(seen[w])
+                    continue
+                prop = LocalFeaturePropagator(csr, rank=p, world_size=P, align=args.align,
+                                              exchange=mode)
+                t = timeit(lambda: prop.propagate(X0, K, output="sharded"), args.reps)
+                ld = (B + 31) // 32 * 32
+                Xw = prop._buf(("h", 0), (n, ld), X0)[:, :w]
+                Yw = prop._buf("send", (P * Bn, B), X0)[:n, :w]
+                hop = timeit(lambda: prop.spmm_fn(Xw, 0, n, Yw, flags=SPMM_X_PADDED | SPMM_Y_PADDED),
+                             args.reps)
+                rows = int(min(n, (p + 1) * Bn) - min(n, p * Bn))
+                outb = torch.empty((rows, F), device="cuda")
+                recv = prop._buf("recv", (P * Bn, B), X0)
+
+                def unpack():
+                    for q in range(P):
+                        q0, q1 = int(fb[q]), int(fb[q + 1])
+                        if q != p and q1 > q0 and rows:
+                            _copy_cols(recv[q * Bn:q * Bn + rows, :q1 - q0], outb[:, q0:q1])
+                t_unpack = timeit(unpack, args.reps)
+                rec = {"case": "rank", "P": P, "exchange": mode, "rank": p, "cols": w,
+                       "compute_ms": t, "hop_ms": hop, "unpack_ms": t_unpack,
+                       "pieces": prop._pieces(P)}
+                if mode == "pairwise":
+                    k = prop._pieces(P)
+                    rec["projected_ms"] = pairwise_projection(t, hop, t_unpack, P, k,
+                                                              Bn * B * 4 / k, args.link_gbps)
+                else:
+                    rec["projected_ms"] = t + a2a / (ingress * 1e9) * 1e3
+                print(json.dumps(rec), flush=True)
+                seen[w] = rec
+                ranks.append(rec)
+                del prop
+                torch.cuda.empty_cache()
+            worst = max(r["compute_ms"] for r in ranks)
+            proj = max(r["projected_ms"] for r in ranks)
+            print(json.dumps({"case": "summary", "P": P, "exchange": mode, "block_floats": B,
+                              "single_ms": t1, "max_rank_compute_ms": worst,
+                              "compute_only_speedup": t1 / worst,
+                              "exchange_MB_per_rank": round(a2a / 1e6, 1),
+                              "link_GBps_each_way": args.link_gbps,
+                              "ingress_GBps": ingress, "projected_step_ms": proj,
+                              "projected_speedup": t1 / proj,
+                              "assumption": "one xGMI link per GPU pair at link_GBps each way; "
+                                            "compute measured on one GPU per rank; pairwise: "
+                                            "sends overlapped with the last hop (timeline model), "
+                                            "alltoall: after it"}), flush=True)
 
 
 if __name__ == "__main__":

@@ -1113,13 +1113,33 @@ class FeaturePartitionedPropagator:
     Every element is still the same single FMA chain in CSR order, so the
     result is bit-identical to one GPU's and to the reference.
 
+    output="sharded" exchanges the row blocks of X_K either with one
+    all-to-all after the last hop (exchange="alltoall") or pairwise, overlapped
+    with the last hop (exchange="pairwise"): rank p computes the rows it owes
+    rank p+1 first, then p+2, ..., its own rows last, and step j of the
+    exchange (send to p+j, receive from p-j; both sides post the same (step,
+    piece) sequence, so the P2P pairs match) is enqueued as soon as its rows
+    are computed, in `pieces` row pieces per destination.  On xGMI every GPU
+    pair has one link, so at P = 2 the all-to-all's 142 MB (Reddit shape)
+    crosses ONE link after the last hop; pairwise, it rides under the
+    computation of the rows that follow.  exchange="auto": pairwise at P = 2
+    only.  Each destination piece is a launch of its own, and a split hop pays
+    every launch's ramp-down tail: measured on one GPU per rank (Reddit shape,
+    profiles/r03/s12/feat.log) the rank's compute grows 5.19 -> 5.74 ms at
+    P = 2 (3 launches), 3.05 -> 3.43 at P = 4, 1.67 -> 2.41 at P = 8, so with
+    one 57.6 GB/s link per GPU pair the projected step is 7.65 -> 6.38 ms at
+    P = 2, 3.66 -> 3.69 at P = 4 and 1.83 -> 2.47 at P = 8.
+
     spmm_fn(X, row_begin, row_end, out) computes rows [row_begin, row_end) of
     S.X for the columns X has; the default is the HIP kernel over the cached
     DeviceCSR (tests inject the CPU oracle to run the exchange over gloo)."""
 
     def __init__(self, csr=None, rank=None, world_size=None, group=None,
                  spmm_fn: Optional[Callable] = None, chunks: int = 4,
-                 host_staging: bool = False, align: int = 4):
+                 host_staging: bool = False, align: int = 4, exchange: str = "auto",
+                 pieces: Optional[int] = None):
+        if exchange not in ("auto", "alltoall", "pairwise"):
+            raise ValueError(f"exchange must be 'auto', 'alltoall' or 'pairwise', not {exchange!r}")
         self.group = group
         self.rank = dist.get_rank(group) if rank is None else int(rank)
         self.world_size = dist.get_world_size(group) if world_size is None else int(world_size)
@@ -1136,6 +1156,8 @@ class FeaturePartitionedPropagator:
         self.chunks = max(1, int(chunks))
         self.align = max(1, int(align))
         self.host_staging = host_staging  # rehearsal only: gathers through host copies (gloo)
+        self.exchange = exchange
+        self.pieces = pieces
         self._bufs = {}
 
     def _buf(self, key, shape, like):
@@ -1160,6 +1182,69 @@ class FeaturePartitionedPropagator:
         dist.all_to_all_single(h_recv, send.cpu(), group=self.group)
         recv.copy_(h_recv)
         return None
+
+    def _global(self, r):
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def _exchange_pair(self, send, dst, recv, src):
+        """One step of the pairwise exchange: send -> rank dst, recv <- rank
+        src (group ranks; an empty side is skipped -- its partner computes the
+        same empty range).  Returns the works to wait on (none when staged)."""
+        staged = self.host_staging
+        h_recv = torch.empty(recv.shape, dtype=recv.dtype) if staged else recv
+        ops = []
+        if send.numel():
+            ops.append(dist.P2POp(dist.isend, send.cpu() if staged else send,
+                                  self._global(dst), group=self.group))
+        if recv.numel():
+            ops.append(dist.P2POp(dist.irecv, h_recv, self._global(src), group=self.group))
+        if not ops:
+            return []
+        works = dist.batch_isend_irecv(ops)
+        if not staged:
+            return works
+        for w_ in works:
+            w_.wait()
+        recv.copy_(h_recv)
+        return []
+
+    def _pieces(self, P):
+        if self.pieces is not None:
+            return max(1, int(self.pieces))
+        return 2 if P == 2 else 1
+
+    def _sharded_pairwise(self, src, own, out, hop, bounds, B, rb, X0):
+        """Last hop + pairwise exchange of the row blocks (class docstring)."""
+        n = X0.shape[0]
+        P, p = self.world_size, self.rank
+        c0, c1 = int(bounds[p]), int(bounds[p + 1])
+        w = c1 - c0
+        Bn = max(1, -(-n // P))
+        send = self._buf("send", (P * Bn, B), X0)
+        recv = self._buf("recv", (P * Bn, B), X0)
+        k = self._pieces(P)
+        mine0, mine1 = int(rb[p]), int(rb[p + 1])
+        works = []
+        for j in range(1, P):
+            q, s_ = (p + j) % P, (p - j) % P
+            q0, q1 = int(rb[q]), int(rb[q + 1])
+            for i in range(k):  # exactly k pieces on both sides (some may be empty)
+                a, b = (q1 - q0) * i // k, (q1 - q0) * (i + 1) // k
+                ra, rb_ = (mine1 - mine0) * i // k, (mine1 - mine0) * (i + 1) // k
+                if w and b > a:  # send's columns w..B-1 are never unpacked: pad-writable
+                    hop(src, q0 + a, q0 + b, send[q0 + a:q0 + b, :w], own, True)
+                works += self._exchange_pair(send[q0 + a:q0 + b], q,
+                                             recv[s_ * Bn + ra:s_ * Bn + rb_], s_)
+        if w and mine1 > mine0:  # own rows straight into the result
+            hop(src, mine0, mine1, out[:, c0:c1], own, False)
+        for w_ in works:
+            w_.wait()
+        rows = mine1 - mine0
+        for s_ in range(P):
+            q0, q1 = int(bounds[s_]), int(bounds[s_ + 1])
+            if s_ != p and q1 > q0 and rows:
+                _copy_cols(recv[s_ * Bn:s_ * Bn + rows, :q1 - q0], out[:, q0:q1])
+        return out
 
     def propagate(self, X0, K, out=None, output="replicated"):
         """output="replicated": the full X_K on every rank (one all-gather).
@@ -1212,6 +1297,9 @@ class FeaturePartitionedPropagator:
             if w and n:
                 hop(src, 0, n, out, own, False)
             return out
+        if output == "sharded" and (self.exchange == "pairwise" or
+                                    (self.exchange == "auto" and P == 2)):
+            return self._sharded_pairwise(src, own, out, hop, bounds, B, rb, X0)
         if output == "sharded":
             # last hop -> one all-to-all.  Destination block q is rows
             # [q*Bn, (q+1)*Bn) (equal_row_bounds), so ONE launch over all rows

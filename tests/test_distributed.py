@@ -340,7 +340,8 @@ def test_row_chunks():
     assert row_chunks(0, 4) == [(0, 0)]
 
 
-def _feature_worker(rank, world, port, case, K, result_q, chunks, align, staging, output):
+def _feature_worker(rank, world, port, case, K, result_q, chunks, align, staging, output,
+                    exchange="auto", pieces=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -352,7 +353,8 @@ def _feature_worker(rank, world, port, case, K, result_q, chunks, align, staging
             out.copy_(torch.from_numpy(o.spmm_csr(rp, ci, va, X.numpy(), r0, r1)))
 
         prop = FeaturePartitionedPropagator(spmm_fn=spmm_fn, chunks=chunks, align=align,
-                                            host_staging=staging)
+                                            host_staging=staging, exchange=exchange,
+                                            pieces=pieces)
         out = prop.propagate(torch.from_numpy(case["X"]), K, output=output)
         out2 = prop.propagate(torch.from_numpy(case["X"]), K, output=output)  # buffers reused
         assert torch.equal(out, out2)
@@ -367,14 +369,21 @@ def _feature_worker(rank, world, port, case, K, result_q, chunks, align, staging
     (4, "hub1000_F130", 2, 2, 4, False, "replicated"),
     (4, "raw_unsorted_dups_F7", 3, 5, 1, False, "sharded"),
     (2, "isolated_F17", 1, 1, 2, True, "replicated"), (3, "norm_n48_F3", 2, 4, 1, True, "sharded")])
+@pytest.mark.parametrize("exchange,pieces", [("auto", None), ("alltoall", None), ("pairwise", 3)])
 def test_feature_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, chunks, align,
-                                          staging, output):
+                                          staging, output, exchange, pieces):
+    """Sharded output: the all-to-all after the last hop, or the pairwise
+    exchange overlapped with it (auto = pairwise at world 2), k row pieces
+    per destination (3 pieces of 16-row blocks: uneven and empty pieces)."""
+    if output == "replicated" and exchange != "auto":
+        pytest.skip("the exchange mode applies to sharded output")
     case = tiny_cases[name]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_feature_worker,
-                         args=(r, world, port, case, K, q, chunks, align, staging, output))
+                         args=(r, world, port, case, K, q, chunks, align, staging, output,
+                               exchange, pieces))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -202,3 +202,21 @@ def test_p8_partition_full_size_bit_exact(dist_cache, shape, partition, extra):
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _last_json(r.stdout)
     assert rec["world"] == 8 and rec["bit_exact_vs_reference_hash"], rec
+
+
+@pytest.mark.slow
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,extra", [
+    (2, ["--exchange", "pairwise"]),
+    (4, ["--exchange", "pairwise", "--pieces", "3"]),
+    (2, ["--exchange", "alltoall"])])
+def test_feature_partition_exchange_full_size_bit_exact(dist_cache, world, extra):
+    """The feature partition's sharded exchange at world 2 / 4 (pairwise P2P
+    overlapped with the last hop, the default at world 2; or the all-to-all), full
+    Reddit shape: X_K assembled from the ranks' row blocks equals the
+    reference's hash."""
+    r = _torchrun(world, ["scripts/dist_check.py", "--shape", "reddit", "--partition", "features",
+                          "--cache", dist_cache, *extra], timeout=540)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _last_json(r.stdout)
+    assert rec["world"] == world and rec["bit_exact_vs_reference_hash"], rec
