@@ -13,7 +13,7 @@
 The workload runs exactly what bench.py times: propagate() (K hops, X_0
 re-laid into 128-B rows, ping-pong buffers, last hop into the caller's
 [N, F] output) on the seeded BASELINE-shape graph, REPEATS times.  Every
-SpMM launch (spmm_csr_kernel + the spmm_hub_kernel dispatches of the same
+SpMM launch (the light kernel + the spmm_hub_kernel dispatches of the same
 call) is one "launch"; the JSON holds the mean bytes per launch.
 
 Calibration (MI355X_MICROARCH.md, HBM section: FETCH_SIZE under-counts wide
@@ -180,12 +180,16 @@ def summarize(out_dir, shape):
     h, m = mean(hit, red_h), mean(miss, red_h)
     kms = _kernel_ms(os.path.join(out_dir, "pmc_fetch"))
     main_ms = [kms[g[0]] for g in red_f if g[0] in kms]
+    names = sorted({fetch[g[0]][0] for g in red_f})
+    # "void sgc::spmm_rows_kernel<16, 2, 16, true>(int const*, ...)" -> "spmm_rows_kernel<16, 2, 16, true>"
+    kname = " / ".join(nm.split("(")[0].replace("void ", "").replace("sgc::", "") for nm in names)
     alg = 4 * (n + 1) + 8 * nnz + 4 * F * nnz + 4 * F * n
     comp = 4 * (n + 1) + 8 * nnz + 8 * F * n
     rec = {
         "workload": f"{shape}-shape propagate() K={K} ({n} rows, {nnz} nnz, F={F}; X_0 in 128-B rows "
                     f"to ld {LD}, intermediates ld {LD}, last hop into ld {F}), {REPEATS} times; "
-                    f"one launch = one hop (spmm_csr_kernel + its spmm_hub_kernel dispatches)",
+                    f"one launch = one hop ({kname} + its spmm_hub_kernel dispatches)",
+        "light_kernel": kname,
         "lib_sha256": meta["lib_sha256"], "tuning": meta["tuning"],
         "hbm_bytes_per_launch": red_fetch_b + red_write_b,
         "hbm_read_bytes_per_launch": red_fetch_b,
@@ -201,7 +205,7 @@ def summarize(out_dir, shape):
                         "identity_S_write_factor": id_write_factor},
         "l2_hit_rate": h / (h + m) if (h + m) > 0 and not math.isnan(h) else None,
         "kernel_ms": (sum(main_ms) / len(main_ms)) if main_ms else None,
-        "kernel_ms_note": "spmm_csr_kernel mean duration in the profiled FETCH_SIZE pass "
+        "kernel_ms_note": f"{kname} mean duration in the profiled FETCH_SIZE pass "
                           "(profiled passes run slower than unprofiled ones)",
         "algorithmic_bytes_per_launch": alg,
         "compulsory_bytes_per_launch": comp,
