@@ -186,9 +186,10 @@ def cpu_baseline(S, X_host, reps=3):
     return rec
 
 
-def load_traffic(shape, lib_sha):
+def load_traffic(shape, lib_sha, groups=1):
     """Measured bytes per hop from profiles/pmc_<shape>.json, or (None, why)
-    when absent or taken on a different build of the library."""
+    when absent or taken on a different build of the library or schedule
+    (column-group dispatches per hop)."""
     p = os.path.join(ROOT, "profiles", f"pmc_{shape}.json")
     if not os.path.exists(p):
         return None, f"no {os.path.relpath(p, ROOT)}"
@@ -197,19 +198,25 @@ def load_traffic(shape, lib_sha):
     if d.get("lib_sha256") != lib_sha:
         return None, (f"{os.path.relpath(p, ROOT)} was taken on libsgc_amd.so "
                       f"{str(d.get('lib_sha256'))[:12]}, not the timed {lib_sha[:12]}: refused")
+    if int(d.get("dispatches_per_launch", 1)) != int(groups):
+        return None, (f"{os.path.relpath(p, ROOT)} counts {d.get('dispatches_per_launch', 1)} "
+                      f"dispatch(es) per hop, the timed schedule {groups}: refused")
     return d, os.path.relpath(p, ROOT)
 
 
-def roofline(shape, n, nnz, F, hop_ms, light_ms, hub_ms, lib_sha, launch_desc, light_kernel):
+def roofline(shape, n, nnz, F, hop_ms, light_ms, hub_ms, lib_sha, launch_desc, light_kernel,
+             groups=1, light_dispatch_ms=None):
     gm = gather_model_bytes(n, nnz, F)
     cb = compulsory_bytes(n, nnz, F)
     t = hop_ms * 1e-3
-    pmc, src = load_traffic(shape, lib_sha)
+    pmc, src = load_traffic(shape, lib_sha, groups)
     rec = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "kernel": (f"{light_kernel} (+ spmm_hub_kernel beside it, joined)" if hub_ms else
                       str(light_kernel)),
            "kernel_mean_ms": hop_ms, "launch_unit": launch_desc,
            "light_kernel_mean_ms": light_ms, "hub_kernel_mean_ms": hub_ms,
+           "dispatches_per_launch": groups,
+           "light_kernel_dispatch_mean_ms": light_dispatch_ms,
            "hub_tail_ms": (max(0.0, hub_ms - light_ms) if hub_ms is not None and light_ms
                            else None),
            "gather_model_bytes_per_launch": gm,
@@ -236,6 +243,10 @@ class LaunchTimer:
     the stream it runs on, and its span as the launch stream sees it (hub
     kernel joined) -- the hop time of the roofline."""
 
+    def __init__(self, groups=1):
+        self.groups = max(1, int(groups))  # dispatches per hop (column groups)
+        self.dispatch_light = []
+
     def start(self):
         collect_launch_timing()  # drop anything recorded before
         kernel_timing(True)
@@ -246,6 +257,14 @@ class LaunchTimer:
         light, hub, span, kind = collect_launch_timing()
         names = [k for k in kind if k]
         top = max(set(names), key=names.count) if names else None
+        self.dispatch_light = list(light)
+        G = self.groups
+        if G > 1:  # a hop = G consecutive launches on one stream: sum them
+            def per_hop(v):
+                return [sum(x or 0.0 for x in v[i:i + G]) for i in range(0, len(v) - G + 1, G)]
+            has_hub = any(h is not None for h in hub)
+            span, light = per_hop(span), per_hop(light)
+            hub = per_hop(hub) if has_hub else []
         return span, light, [h for h in hub if h is not None], top
 
 
@@ -292,7 +311,8 @@ def single_gpu_shape(shape, args, dev, lib_sha, steps, warmup, S=None, X_host=No
     adjacency whose CSR it caches on the first call (as reddit.py's repeated
     calls would) -- throughput, per-kernel times, roofline and the first-call
     (ingest + plan + propagation) time."""
-    from sgc_amd import propagate as prop_mod
+    import importlib
+    prop_mod = importlib.import_module("sgc_amd.propagate")
     from sgc_amd.utils import sgc_precompute
     if args.threshold is not None:
         prop_mod.DEFAULT_HEAVY_THRESHOLD = args.threshold
@@ -316,7 +336,8 @@ def single_gpu_shape(shape, args, dev, lib_sha, steps, warmup, S=None, X_host=No
     torch.cuda.synchronize()
     _, first_s = sgc_precompute(X0, adj, K)
     ingest_s = adj._sgc_amd_csr[1].ingest_seconds
-    launches = LaunchTimer()
+    groups = prop_mod.column_groups_for(adj._sgc_amd_csr[1], F)
+    launches = LaunchTimer(groups)
 
     def step():  # the public call, as the reference's drivers make it
         return sgc_precompute(X0, adj, K)[0]
@@ -340,7 +361,10 @@ def single_gpu_shape(shape, args, dev, lib_sha, steps, warmup, S=None, X_host=No
            "first_call_seconds": round(first_s, 4), "ingest_seconds": round(ingest_s, 4),
            "generate_seconds": round(t_gen, 2),
            "roofline": roofline(shape, n, nnz, F, hop_mean, mean_or_none(light),
-                                mean_or_none(hub), lib_sha, f"one hop over all {n} rows", kernel),
+                                mean_or_none(hub), lib_sha,
+                                f"one hop over all {n} rows" + (
+                                    f" = {groups} column-group dispatches" if groups > 1 else ""),
+                                kernel, groups, mean_or_none(launches.dispatch_light)),
            "hop_ms_median": float(np.median(hop_ms)),
            "timed_call": "sgc_precompute(features, adj, K) (sgc_amd.utils, the drop-in)"}
     del X0, adj

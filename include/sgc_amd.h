@@ -355,6 +355,29 @@ int sgc_plan_sorted(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
                     int64_t workspace_bytes, int64_t *counts_host, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Column groups of S (a schedule for the SpMM of utils.py:95; results
+ * unchanged).  Splits every row's nonzeros at the column cuts
+ * 0 = cuts[0] <= cuts[1] <= ... <= cuts[G] = n_cols into G CSRs over the same
+ * rows.  REQUIRES rows whose columns do not decrease (sgc_coo_to_csr status
+ * bit 2): group g's part of a row is then one contiguous run, the runs come
+ * in group order, and a hop computed as G launches -- group 0 plain, groups
+ * 1.. with SGC_SPMM_ACCUMULATE -- applies every row's FMAs in CSR order: the
+ * same bits as one launch, while each launch gathers only its group's X rows
+ * (a live X slice 1/G as large, more of it in the per-XCD L2s).
+ *   row_ptrs: [G][n_rows+1] int32, group g's row_ptr at row_ptrs + g*(n_rows+1),
+ *             absolute offsets into col_out/val_out (groups stored one after
+ *             the other), so (row_ptrs + g*(n_rows+1), col_out, val_out) is an
+ *             ordinary CSR for sgc_spmm_csr_f32_ex / sgc_plan_sorted;
+ *   col_out / val_out: [nnz];  G <= 8;  asynchronous on `stream`;
+ *   workspace: sgc_colsplit_workspace(n_rows, G) bytes on the device.
+ * ------------------------------------------------------------------------- */
+int64_t sgc_colsplit_workspace(int64_t n_rows, int32_t groups);
+int sgc_csr_colsplit(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                     int64_t n_rows, int64_t n_cols, int32_t groups, const int32_t *cuts_host,
+                     int32_t *row_ptrs, int32_t *col_out, float *val_out, void *workspace,
+                     int64_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------
  * One process, several GPUs (the multi-GPU form of the one
  * call reddit.py:43 makes, sgc_precompute -> utils.py:92-97).  The engine
  * splits the feature columns over the devices: device d pulls its column

@@ -63,7 +63,7 @@ def workload(shape):
 
     from sgc_amd import _lib, graphs
     from sgc_amd.propagate import (SPMM_X_PADDED, SPMM_Y_PADDED, DeviceCSR, aligned_ld,
-                                   propagate, spmm)
+                                   column_groups_for, propagate, spmm)
     dev = torch.device("cuda", 0)
     spec = graphs.SHAPES[shape]
     F, K = spec["features"], spec["hops"]
@@ -97,7 +97,8 @@ def workload(shape):
     tuning = {k: int(lib.sgc_get_tuning(k.encode())) for k in TUNING_KEYS}
     with open(_meta_path(shape), "w") as f:
         json.dump({"shape": shape, "n": S.n, "nnz": S.nnz, "F": F, "K": K, "ld": LD,
-                   "n_cal": N_CAL, "lib_sha256": lib_sha(), "tuning": tuning}, f)
+                   "n_cal": N_CAL, "lib_sha256": lib_sha(), "tuning": tuning,
+                   "groups": column_groups_for(csr, F)}, f)
     print(f"pmc workload done: {shape} {S.nnz} nnz, K={K}, tuning {tuning}")
 
 
@@ -139,16 +140,21 @@ def _per_dispatch(rows, counter):
     return acc
 
 
-def _launches(d, K):
+def _launches(d, K, G=1):
     """(identity-calibration ids, permutation-calibration ids,
-    [[main id, hub ids...] per shape launch])."""
+    [[main ids..., hub ids...] per hop]): a hop is G column-group dispatches
+    of the light kernel and the hub dispatches among them."""
     ks = sorted(k for k, (nm, _) in d.items()
                 if "spmm_csr_kernel" in nm or "spmm_rows_kernel" in nm)
     hubs = sorted(k for k, (nm, _) in d.items() if "spmm_hub_kernel" in nm)
     cal_id, cal_perm = ks[:REPEATS], ks[REPEATS:2 * REPEATS]
-    main = ks[2 * REPEATS:2 * REPEATS + REPEATS * K]
-    prev = [cal_perm[-1]] + main[:-1]
-    return cal_id, cal_perm, [[k] + [h for h in hubs if p < h < k] for p, k in zip(prev, main)]
+    main = ks[2 * REPEATS:2 * REPEATS + REPEATS * K * G]
+    out, prev = [], cal_perm[-1]
+    for i in range(0, len(main), G):
+        grp = main[i:i + G]
+        out.append(grp + [h for h in hubs if prev < h < grp[-1]])
+        prev = grp[-1]
+    return cal_id, cal_perm, out
 
 
 def summarize(out_dir, shape):
@@ -159,9 +165,10 @@ def summarize(out_dir, shape):
     write = _per_dispatch(_rows(os.path.join(out_dir, "pmc_write")), "WRITE_SIZE")
     l2 = _rows(os.path.join(out_dir, "pmc_l2"))
     hit, miss = _per_dispatch(l2, "TCC_HIT_sum"), _per_dispatch(l2, "TCC_MISS_sum")
-    calid_f, cal_f, red_f = _launches(fetch, K)
-    calid_w, cal_w, red_w = _launches(write, K)
-    _, _, red_h = _launches(hit, K)
+    G = int(meta.get("groups", 1))
+    calid_f, cal_f, red_f = _launches(fetch, K, G)
+    calid_w, cal_w, red_w = _launches(write, K, G)
+    _, _, red_h = _launches(hit, K, G)
 
     def mean(d, ks):
         vals = [sum(d[j][1] for j in k) if isinstance(k, list) else d[k][1] for k in ks]
@@ -179,7 +186,7 @@ def summarize(out_dir, shape):
     red_write_b = mean(write, red_w) * 1024 * write_factor
     h, m = mean(hit, red_h), mean(miss, red_h)
     kms = _kernel_ms(os.path.join(out_dir, "pmc_fetch"))
-    main_ms = [kms[g[0]] for g in red_f if g[0] in kms]
+    main_ms = [sum(kms[k] for k in g[:G]) for g in red_f if all(k in kms for k in g[:G])]
     names = sorted({fetch[g[0]][0] for g in red_f})
     # "void sgc::spmm_rows_kernel<16, 2, 16, true>(int const*, ...)" -> "spmm_rows_kernel<16, 2, 16, true>"
     kname = " / ".join(nm.split("(")[0].replace("void ", "").replace("sgc::", "") for nm in names)
@@ -188,7 +195,9 @@ def summarize(out_dir, shape):
     rec = {
         "workload": f"{shape}-shape propagate() K={K} ({n} rows, {nnz} nnz, F={F}; X_0 in 128-B rows "
                     f"to ld {LD}, intermediates ld {LD}, last hop into ld {F}), {REPEATS} times; "
-                    f"one launch = one hop ({kname} + its spmm_hub_kernel dispatches)",
+                    f"one launch = one hop ({G} column-group dispatch(es) of {kname} + the "
+                    f"spmm_hub_kernel dispatches among them)",
+        "dispatches_per_launch": G,
         "light_kernel": kname,
         "lib_sha256": meta["lib_sha256"], "tuning": meta["tuning"],
         "hbm_bytes_per_launch": red_fetch_b + red_write_b,
@@ -205,7 +214,8 @@ def summarize(out_dir, shape):
                         "identity_S_write_factor": id_write_factor},
         "l2_hit_rate": h / (h + m) if (h + m) > 0 and not math.isnan(h) else None,
         "kernel_ms": (sum(main_ms) / len(main_ms)) if main_ms else None,
-        "kernel_ms_note": f"{kname} mean duration in the profiled FETCH_SIZE pass "
+        "kernel_ms_note": f"{kname}: sum of a hop's {G} dispatch durations, mean over hops, in "
+                          "the profiled FETCH_SIZE pass "
                           "(profiled passes run slower than unprofiled ones)",
         "algorithmic_bytes_per_launch": alg,
         "compulsory_bytes_per_launch": comp,

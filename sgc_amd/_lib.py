@@ -67,6 +67,9 @@ SIGNATURES = {
     "sgc_propagate_cpu_workspace": (_i64, [_i64, _i64, _i32]),
     "sgc_propagate_f32_cpu": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _i32,
                                              _p, _i64, _i32]),
+    "sgc_colsplit_workspace": (_i64, [_i64, _i32]),
+    "sgc_csr_colsplit": (ctypes.c_int, [_p, _p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _i64,
+                                        _p]),
     "sgc_plan_sorted_workspace": (_i64, [_i64]),
     "sgc_plan_sorted": (ctypes.c_int, [_p, _i64, _i64, _i32, _i32, _p, _p, _i64, _p, _p]),
     "sgc_mgpu_init": (ctypes.c_int, [ctypes.c_int, _p]),

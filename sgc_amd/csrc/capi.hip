@@ -77,6 +77,11 @@ int64_t plan_sorted_workspace(int64_t n_rows);
 int plan_sorted(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int32_t threshold,
                 int32_t hub_threshold, int32_t *plan, void *workspace, int64_t workspace_bytes,
                 int64_t *counts_host, hipStream_t stream);
+int64_t colsplit_workspace(int64_t n_rows, int32_t groups);
+int colsplit(const int32_t *row_ptr, const int32_t *col_idx, const float *val, int64_t n_rows,
+             int64_t n_cols, int32_t groups, const int32_t *cuts_host, int32_t *row_ptrs,
+             int32_t *col_out, float *val_out, void *workspace, int64_t workspace_bytes,
+             hipStream_t stream);
 int mgpu_init(int ndev, const int *devices);
 int mgpu_finalize();
 int mgpu_attach(const int32_t *row_ptr, const int32_t *col_idx, const float *val, int64_t n,
@@ -361,6 +366,18 @@ int sgc_mgpu_propagate(int64_t handle, const float *X0, int64_t ldx, float *out,
 int sgc_mgpu_detach(int64_t handle) { return mgpu_detach(handle); }
 
 int sgc_mgpu_finalize(void) { return mgpu_finalize(); }
+
+int64_t sgc_colsplit_workspace(int64_t n_rows, int32_t groups) {
+    return colsplit_workspace(n_rows, groups);
+}
+
+int sgc_csr_colsplit(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                     int64_t n_rows, int64_t n_cols, int32_t groups, const int32_t *cuts_host,
+                     int32_t *row_ptrs, int32_t *col_out, float *val_out, void *workspace,
+                     int64_t workspace_bytes, void *stream) {
+    return colsplit(row_ptr, col_idx, val, n_rows, n_cols, groups, cuts_host, row_ptrs, col_out,
+                    val_out, workspace, workspace_bytes, as_stream(stream));
+}
 
 int64_t sgc_plan_sorted_workspace(int64_t n_rows) { return plan_sorted_workspace(n_rows); }
 

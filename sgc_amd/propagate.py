@@ -11,6 +11,7 @@ import os
 from dataclasses import dataclass, field
 from typing import NamedTuple, Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -104,6 +105,55 @@ STATUS_ROWS_SORTED = 1
 STATUS_COLS_ASCENDING = 2
 STATUS_OUT_OF_RANGE = 4
 
+# Column groups (sgc_csr_colsplit): one hop as G launches over the same rows,
+# group 0 plain and groups 1.. accumulating, each gathering only the X rows
+# of its column range -- the live X slice is 1/G as large and more of it stays
+# in the per-XCD L2s.  Same bits (rows with ascending columns only).  Measured
+# one hop, interleaved, bit-identical (profiles/r03/s14/colgroup*.log):
+# Reddit shape at 602 floats 4.30 -> 3.83 ms (G = 2; 3.81 at 3, 3.88 at 4, 4.73
+# at 8), at 304 2.45 -> 2.29, at 128 0.95 -> 0.84, at 76 0.77 -> 0.77, at
+# 152 / 256 (the one-row kernel) 1.56 -> 1.58 / 1.85 -> 1.88;
+# RMAT shape (F = 256) 31.4 -> 30.1 (G = 2) -> 29.5 ms (G = 4).  None set =
+# column_groups_for's size rule; SGC_AMD_COLUMN_GROUPS=G forces G (1 = off).
+_GROUPS_ENV = os.environ.get("SGC_AMD_COLUMN_GROUPS")
+COLUMN_GROUPS = int(_GROUPS_ENV) if _GROUPS_ENV else None
+GROUPS_MIN_NNZ = 1 << 22    # below: latency-bound launches, one launch per hop
+GROUPS_MIN_WIDTH = 128      # narrower launches gain nothing (76 floats: 0.77 vs 0.77 ms)
+GROUPS_WIDE_NNZ = 1 << 26   # from here four groups (RMAT shape)
+
+
+def column_groups_for(csr, width):
+    """Column groups for a plain launch of `width` features over `csr`."""
+    if csr.device.type != "cuda" or not csr.cols_ascending or csr.nnz == 0:
+        return 1
+    if COLUMN_GROUPS is not None:
+        return max(1, min(8, int(COLUMN_GROUPS), max(1, csr.n_cols)))
+    if width < GROUPS_MIN_WIDTH or csr.nnz < GROUPS_MIN_NNZ:
+        return 1
+    if csr.nnz >= GROUPS_WIDE_NNZ:
+        return 4
+    if 128 < width <= 256:  # the one-row kernel's single 256-float slice: no gain
+        return 1            # (152 floats 1.56 -> 1.58 ms, 256 1.85 -> 1.88 at G = 2)
+    return 2
+
+
+def _host_cols_ascending(row_ptr, col_idx):
+    """Every row's columns strictly ascending?  (host arrays; False for
+    anything else, which only turns the column groups off)."""
+    if isinstance(row_ptr, torch.Tensor):
+        if row_ptr.device.type != "cpu" or col_idx.device.type != "cpu":
+            return False
+        row_ptr, col_idx = row_ptr.numpy(), col_idx.numpy()
+    rp = np.asarray(row_ptr, dtype=np.int64)
+    ci = np.asarray(col_idx)
+    if ci.size < 2:
+        return True
+    bad = np.diff(ci.astype(np.int64)) <= 0  # bad[k-1]: col[k] <= col[k-1]
+    starts = rp[1:-1]
+    starts = starts[(starts > 0) & (starts < ci.size)]
+    bad[starts - 1] = False  # k is a row's first nonzero: no predecessor in its row
+    return not bool(bad.any())
+
 
 def _require_device(t, what):
     if not isinstance(t, torch.Tensor):
@@ -144,15 +194,51 @@ class DeviceCSR:
     def device(self):
         return self.row_ptr.device
 
+    @property
+    def cols_ascending(self):
+        """Every row's columns strictly ascending (the ingest's status bit)."""
+        return bool(self.status & STATUS_COLS_ASCENDING)
+
+    def column_groups(self, G):
+        """The G column-group CSRs of this one (sgc_csr_colsplit; cached):
+        columns cut at g * n_cols / G, every row's run of each group in its
+        storage order; group g's row_ptr points into one shared col/val
+        copy.  Rows must have ascending columns."""
+        if not self.cols_ascending:
+            raise ValueError("sgc_amd: column groups need rows with ascending columns")
+        key = ("groups", int(G))
+        if key not in self._plans:
+            import ctypes
+            lib = _lib.load()
+            n, nnz, dev = self.n_rows, self.nnz, self.device
+            cuts = (ctypes.c_int32 * (G + 1))(*[(g * self.n_cols) // G for g in range(G + 1)])
+            row_ptrs = torch.empty((G, n + 1), dtype=torch.int32, device=dev)
+            col = torch.empty(max(1, nnz), dtype=torch.int32, device=dev)
+            val = torch.empty(max(1, nnz), dtype=torch.float32, device=dev)
+            ws_bytes = lib.sgc_colsplit_workspace(n, G)
+            ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8, device=dev)
+            with torch.cuda.device(dev):
+                _lib.check(lib.sgc_csr_colsplit(_lib.ptr(self.row_ptr), _lib.ptr(self.col_idx),
+                                                _lib.ptr(self.val), n, self.n_cols, G,
+                                                ctypes.cast(cuts, ctypes.c_void_p),
+                                                _lib.ptr(row_ptrs), _lib.ptr(col), _lib.ptr(val),
+                                                _lib.ptr(ws), ws_bytes,
+                                                _lib.stream_handle(dev)), "csr_colsplit")
+            del ws  # stream-ordered: the allocator reuses it after the kernels
+            self._plans[key] = [DeviceCSR(n, self.n_cols, row_ptrs[g], col[:nnz], val[:nnz],
+                                          self.status) for g in range(G)]
+        return self._plans[key]
+
     @classmethod
     def from_host_arrays(cls, row_ptr, col_idx, val, n_cols=None, device="cuda"):
         """From host CSR arrays already in the SpMM's order (numpy or torch)."""
+        status = STATUS_COLS_ASCENDING if _host_cols_ascending(row_ptr, col_idx) else 0
         rp = torch.as_tensor(row_ptr).to(device=device, dtype=torch.int32)
         ci = torch.as_tensor(col_idx).to(device=device, dtype=torch.int32)
         va = torch.as_tensor(val).to(device=device, dtype=torch.float32)
         n = rp.numel() - 1
         return cls(n, n if n_cols is None else n_cols, rp.contiguous(), ci.contiguous(),
-                   va.contiguous())
+                   va.contiguous(), status)
 
     @classmethod
     def from_torch(cls, adj):
@@ -414,15 +500,22 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
                                                out.stride(0), F, int(flags) & ~SPMM_NO_HUB,
                                                cpu_threads()), "spmm_csr_f32_cpu")
         return out
-    pl = csr.plan(row_begin, row_end, threshold, hub_threshold, F) if use_plan else NO_PLAN
+    G = 1
+    if use_plan and not flags & (SPMM_ACCUMULATE | SPMM_NO_HUB | SPMM_HUB_ONLY):
+        G = column_groups_for(csr, F)
+    parts = csr.column_groups(G) if G > 1 else [csr]
     with torch.cuda.device(X.device):
-        _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
-                                           _lib.ptr(csr.val), row_begin, row_end, _lib.ptr(X),
-                                           X.stride(0), _lib.ptr(out), out.stride(0), F,
-                                           _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
-                                           int(flags) | pl.hub_flags() | x_flags(X),
-                                           _lib.stream_handle(X.device)),
-                   "spmm_csr_f32")
+        stream = _lib.stream_handle(X.device)
+        for g, c in enumerate(parts):  # group 0 plain, groups 1.. continue its chains
+            pl = c.plan(row_begin, row_end, threshold, hub_threshold, F) if use_plan else NO_PLAN
+            _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(c.row_ptr), _lib.ptr(c.col_idx),
+                                               _lib.ptr(c.val), row_begin, row_end, _lib.ptr(X),
+                                               X.stride(0), _lib.ptr(out), out.stride(0), F,
+                                               _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub,
+                                               pl.threshold,
+                                               int(flags) | pl.hub_flags() | x_flags(X) |
+                                               (SPMM_ACCUMULATE if g else 0), stream),
+                       "spmm_csr_f32")
     return out
 
 
@@ -509,6 +602,9 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                                              ws_bytes, cpu_threads()), "propagate_f32_cpu")
         return out
     pl = csr.plan(0, n, threshold, hub_threshold, F) if use_plan else NO_PLAN
+    G = column_groups_for(csr, F) if use_plan and not native_loop else 1
+    parts = [(c, c.plan(0, n, threshold, hub_threshold, F)) for c in csr.column_groups(G)] \
+        if G > 1 else [(csr, pl)]
     stream = _lib.stream_handle(X.device)
     ldw = aligned_ld(F)
     with torch.cuda.device(X.device):
@@ -539,11 +635,15 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                      (SPMM_Y_PADDED if dst is not out else 0) | pl.hub_flags() | x_flags(src))
             if hop_hook:
                 hop_hook("start", h)
-            _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
-                                               _lib.ptr(csr.val), 0, n, _lib.ptr(src),
-                                               src.stride(0), _lib.ptr(dst), dst.stride(0), F,
-                                               _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub,
-                                               pl.threshold, flags, stream), "spmm_csr_f32")
+            for g, (c, cp) in enumerate(parts):  # column groups: 0 plain, 1.. accumulate
+                _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(c.row_ptr), _lib.ptr(c.col_idx),
+                                                   _lib.ptr(c.val), 0, n, _lib.ptr(src),
+                                                   src.stride(0), _lib.ptr(dst), dst.stride(0),
+                                                   F, _lib.ptr(cp.rows), cp.n_heavy, cp.n_hub,
+                                                   cp.threshold,
+                                                   (flags & ~pl.hub_flags()) | cp.hub_flags() |
+                                                   (SPMM_ACCUMULATE if g else 0), stream),
+                           "spmm_csr_f32")
             if hop_hook:
                 hop_hook("end", h)
             src, nxt = dst, nxt ^ 1

@@ -34,11 +34,15 @@ def test_roofline_uses_matching_pmc_record(shape):
     path = os.path.join(ROOT, "profiles", f"pmc_{shape}.json")
     pmc = json.load(open(path))
     pmc_sha = pmc["lib_sha256"]
-    traffic, src = bench.load_traffic(shape, pmc_sha)
+    G = int(pmc.get("dispatches_per_launch", 1))
+    traffic, src = bench.load_traffic(shape, pmc_sha, G)
     assert traffic is not None and traffic["hbm_bytes_per_launch"] > 0
+    # a record of another schedule (column-group dispatches per hop) is refused
+    other, why = bench.load_traffic(shape, pmc_sha, G + 1)
+    assert other is None and "refused" in why
     ms = float(pmc["kernel_ms"])  # the hop time the counters were taken over
     rec = bench.roofline(shape, REDDIT["n"], REDDIT["nnz"], REDDIT["F"], ms, ms, None,
-                         pmc_sha, "one hop", "spmm_rows_kernel")
+                         pmc_sha, "one hop", "spmm_rows_kernel", G)
     t = ms * 1e-3
     assert rec["traffic"] == traffic["hbm_bytes_per_launch"]
     assert rec["frac"] == pytest.approx(rec["traffic"] / t / 1e9 / bench.HBM_PEAK_GBS)
@@ -58,3 +62,15 @@ def test_self_launch_refuses_more_ranks_than_gpus(monkeypatch, capsys):
     args = argparse.Namespace(gpus=4, dist_backend="nccl")
     assert bench.self_launch(args) == 2
     assert "needs 4 GPUs" in capsys.readouterr().err
+
+
+def test_host_cols_ascending():
+    """The host check that turns column groups on for from_host_arrays CSRs:
+    strictly ascending columns within every row (empty rows allowed)."""
+    import numpy as np
+    from sgc_amd.propagate import _host_cols_ascending as asc
+    assert asc(np.array([0, 2, 2, 5]), np.array([1, 3, 0, 2, 9]))
+    assert not asc(np.array([0, 2, 2, 5]), np.array([1, 3, 0, 2, 2]))  # duplicate
+    assert not asc(np.array([0, 2, 5]), np.array([3, 1, 0, 2, 9]))     # descending
+    assert asc(np.array([0, 0, 0]), np.array([], dtype=np.int32))
+    assert asc(np.array([0, 1, 2]), np.array([5, 0]))                    # one per row

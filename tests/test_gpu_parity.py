@@ -647,3 +647,96 @@ def test_plan_sorted_matches_host_plan(r0, r1, th, hub):
     want = (np.argsort(-d, kind="stable") + r0).astype(np.int32)
     assert list(counts) == [int((d > th).sum()), int((d > hub).sum()), int(d.max()) if n else 0]
     assert np.array_equal(out[:n].cpu().numpy(), want)
+
+
+# ---------------------------------------------------------------------------
+# Column groups: one hop as G launches over column ranges (accumulating).
+
+def _split_host(rp, ci, va, n_cols, G):
+    """Reference split for sgc_csr_colsplit: group-major arrays, absolute row_ptrs."""
+    n = rp.shape[0] - 1
+    cuts = [(g * n_cols) // G for g in range(G + 1)]
+    rps, cols, vals, base = [], [], [], 0
+    row = np.repeat(np.arange(n), np.diff(rp))
+    for g in range(G):
+        keep = (ci >= cuts[g]) & (ci < cuts[g + 1])
+        cnt = np.bincount(row[keep], minlength=n)
+        rps.append(base + np.concatenate([[0], np.cumsum(cnt)]))
+        cols.append(ci[keep])
+        vals.append(va[keep])
+        base += int(keep.sum())
+    return np.stack(rps).astype(np.int32), np.concatenate(cols), np.concatenate(vals)
+
+
+@pytest.mark.parametrize("G", [2, 3, 5, 8])
+def test_colsplit_matches_host_split(G):
+    """sgc_csr_colsplit: each group's row_ptr (absolute offsets) and the
+    group-major col / val arrays equal a host split at cuts g * n_cols / G
+    (rows with empty groups, a 3,000-nonzero hub, empty rows)."""
+    from sgc_amd import graphs
+    from sgc_amd.propagate import DeviceCSR
+    S = graphs.synthetic_graph("cora", seed=G, n=3000, edges=20000)
+    rp = S.row_ptr.astype(np.int64).copy()
+    ci, va = S.col_idx.copy(), S.val.copy()
+    csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=DEV)
+    assert csr.cols_ascending
+    subs = csr.column_groups(G)
+    torch.cuda.synchronize()
+    want_rp, want_ci, want_va = _split_host(rp, ci, va, S.n, G)
+    for g in range(G):
+        assert np.array_equal(subs[g].row_ptr.cpu().numpy(), want_rp[g]), g
+    assert np.array_equal(subs[0].col_idx.cpu().numpy(), want_ci)
+    assert bits_equal(subs[0].val.cpu().numpy(), want_va)
+
+
+@pytest.mark.parametrize("G", [2, 3, 4, 8])
+def test_column_groups_tiny_cases_bit_exact(tiny_cases, G, monkeypatch):
+    """propagate() and sgc_precompute() with G column groups forced: every
+    golden case bit-exact; cases whose rows are not strictly ascending (raw
+    COO with duplicates / unsorted) run one launch per hop instead."""
+    import importlib
+    prop_mod = importlib.import_module("sgc_amd.propagate")
+    from sgc_amd.propagate import DeviceCSR, column_groups_for, propagate
+    monkeypatch.setattr(prop_mod, "COLUMN_GROUPS", G)
+    for name, c in tiny_cases.items():
+        csr = DeviceCSR.from_torch(coo_cuda(c))
+        X = torch.from_numpy(c["X"]).to(DEV)
+        if csr.cols_ascending and csr.nnz:
+            assert column_groups_for(csr, X.shape[1]) == min(G, csr.n_cols)
+        else:
+            assert column_groups_for(csr, X.shape[1]) == 1
+        for key in sorted(k for k in c if k.startswith("Y") and k != "Y0"):
+            out = propagate(csr, X, int(key[1:]))
+            torch.cuda.synchronize()
+            assert bits_equal(out.cpu().numpy(), c[key]), (name, key, G)
+
+
+@pytest.mark.parametrize("F", [602, 304, 128, 256])
+def test_column_groups_medium_graph_bit_exact(oracle, F):
+    """The default rule on a 4.2 M-nonzero graph (two groups at 128 and
+    > 256 floats, one at 129-256), forced 1, 3 and 4 groups, split hops (spmm over a row range) and
+    the one-launch schedule: the oracle's bits."""
+    from sgc_amd import graphs
+    import importlib
+    prop_mod = importlib.import_module("sgc_amd.propagate")
+    from sgc_amd.propagate import DeviceCSR, column_groups_for, propagate, spmm
+    n = 60000
+    S = graphs.synthetic_graph("pubmed", seed=11, n=n, edges=2_100_000)
+    assert S.nnz >= prop_mod.GROUPS_MIN_NNZ
+    X = np.random.default_rng(F).standard_normal((n, F)).astype(np.float32)
+    want1 = oracle.spmm_csr(S.row_ptr, S.col_idx, S.val, X, 0, n)
+    want2 = oracle.spmm_csr(S.row_ptr, S.col_idx, S.val, want1, 0, n)
+    csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=DEV)
+    Xd = torch.from_numpy(X).to(DEV)
+    assert column_groups_for(csr, F) == (1 if 128 < F <= 256 else 2)
+    saved = prop_mod.COLUMN_GROUPS
+    try:
+        for G in (None, 1, 3, 4):
+            prop_mod.COLUMN_GROUPS = G
+            out = propagate(csr, Xd, 2)
+            part = spmm(csr, Xd, 1000, 37000)
+            torch.cuda.synchronize()
+            assert bits_equal(out.cpu().numpy(), want2), (F, G)
+            assert bits_equal(part.cpu().numpy(), want1[1000:37000]), (F, G)
+    finally:
+        prop_mod.COLUMN_GROUPS = saved
