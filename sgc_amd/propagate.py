@@ -601,10 +601,16 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                                              _lib.ptr(out), out.stride(0), F, int(K), _lib.ptr(ws),
                                              ws_bytes, cpu_threads()), "propagate_f32_cpu")
         return out
-    pl = csr.plan(0, n, threshold, hub_threshold, F) if use_plan else NO_PLAN
     G = column_groups_for(csr, F) if use_plan and not native_loop else 1
-    parts = [(c, c.plan(0, n, threshold, hub_threshold, F)) for c in csr.column_groups(G)] \
-        if G > 1 else [(csr, pl)]
+    if G > 1:
+        pl = None
+        parts = [(c, c.plan(0, n, threshold, hub_threshold, F)) for c in csr.column_groups(G)]
+    else:
+        pl = csr.plan(0, n, threshold, hub_threshold, F) if use_plan else NO_PLAN
+        parts = [(csr, pl)]
+    # (csr, plan, launch flags of the group): groups 1.. continue group 0's chains
+    parts = [(c, cp, cp.hub_flags() | (SPMM_ACCUMULATE if g else 0))
+             for g, (c, cp) in enumerate(parts)]
     stream = _lib.stream_handle(X.device)
     ldw = aligned_ld(F)
     with torch.cuda.device(X.device):
@@ -632,17 +638,15 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
             dst = out if h == K - 1 else bufs[nxt][:, :F]
             # the engine's own buffers may be read / written in their pad columns
             flags = ((SPMM_X_PADDED if src is not X else 0) |
-                     (SPMM_Y_PADDED if dst is not out else 0) | pl.hub_flags() | x_flags(src))
+                     (SPMM_Y_PADDED if dst is not out else 0) | x_flags(src))
             if hop_hook:
                 hop_hook("start", h)
-            for g, (c, cp) in enumerate(parts):  # column groups: 0 plain, 1.. accumulate
+            for c, cp, gflags in parts:  # column groups: 0 plain, 1.. accumulate
                 _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(c.row_ptr), _lib.ptr(c.col_idx),
                                                    _lib.ptr(c.val), 0, n, _lib.ptr(src),
                                                    src.stride(0), _lib.ptr(dst), dst.stride(0),
                                                    F, _lib.ptr(cp.rows), cp.n_heavy, cp.n_hub,
-                                                   cp.threshold,
-                                                   (flags & ~pl.hub_flags()) | cp.hub_flags() |
-                                                   (SPMM_ACCUMULATE if g else 0), stream),
+                                                   cp.threshold, flags | gflags, stream),
                            "spmm_csr_f32")
             if hop_hook:
                 hop_hook("end", h)
