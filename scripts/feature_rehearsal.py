@@ -91,6 +91,7 @@ def main():
                     help="per-peer xGMI rate each way (one link per GPU pair): a rank's "
                          "ingress is (P-1) x this")
     ap.add_argument("--exchange", default="alltoall,pairwise")
+    ap.add_argument("--pieces", type=int, default=None, help="pairwise: row pieces per destination")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="schedule knob for sgc_set_tuning (results never depend on it)")
     args = ap.parse_args()
@@ -122,7 +123,7 @@ def main():
                     ranks.append(seen[w])
                     continue
                 prop = LocalFeaturePropagator(csr, rank=p, world_size=P, align=args.align,
-                                              exchange=mode)
+                                              exchange=mode, pieces=args.pieces)
                 t = timeit(lambda: prop.propagate(X0, K, output="sharded"), args.reps)
                 ld = (B + 31) // 32 * 32
                 Xw = prop._buf(("h", 0), (n, ld), X0)[:, :w]

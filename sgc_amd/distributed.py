@@ -1119,8 +1119,9 @@ class FeaturePartitionedPropagator:
     rank p+1 first, then p+2, ..., its own rows last, and step j of the
     exchange (send to p+j, receive from p-j; both sides post the same (step,
     piece) sequence, so the P2P pairs match) is enqueued as soon as its rows
-    are computed, in `pieces` row pieces per destination.  On xGMI every GPU
-    pair has one link, so at P = 2 the all-to-all's 142 MB (Reddit shape)
+    are computed, in `pieces` row pieces per destination (default 4 at
+    P = 2).  On xGMI every GPU pair has one link, so at P = 2 the
+    all-to-all's 142 MB (Reddit shape)
     crosses ONE link after the last hop; pairwise, it rides under the
     computation of the rows that follow.  exchange="auto": pairwise at P = 2
     only.  Each destination piece is a launch of its own, and a split hop pays
@@ -1128,7 +1129,8 @@ class FeaturePartitionedPropagator:
     profiles/r03/s12/feat.log) the rank's compute grows 5.19 -> 5.74 ms at
     P = 2 (3 launches), 3.05 -> 3.43 at P = 4, 1.67 -> 2.41 at P = 8, so with
     one 57.6 GB/s link per GPU pair the projected step is 7.65 -> 6.38 ms at
-    P = 2, 3.66 -> 3.69 at P = 4 and 1.83 -> 2.47 at P = 8.
+    P = 2, 3.66 -> 3.69 at P = 4 and 1.83 -> 2.47 at P = 8 (with the column
+    groups and 4 pieces at P = 2: 7.40 -> 6.08 ms, profiles/r03/s17/).
 
     spmm_fn(X, row_begin, row_end, out) computes rows [row_begin, row_end) of
     S.X for the columns X has; the default is the HIP kernel over the cached
@@ -1211,7 +1213,10 @@ class FeaturePartitionedPropagator:
     def _pieces(self, P):
         if self.pieces is not None:
             return max(1, int(self.pieces))
-        return 2 if P == 2 else 1
+        # P = 2 over one link: 4 pieces per destination (projected, one GPU per
+        # rank: 6.65 / 6.40 / 6.16 / 6.08 / 6.34 ms at 1 / 2 / 3 / 4 / 6 pieces,
+        # profiles/r03/s17/feat_p2_pieces*.log)
+        return 4 if P == 2 else 1
 
     def _sharded_pairwise(self, src, own, out, hop, bounds, B, rb, X0):
         """Last hop + pairwise exchange of the row blocks (class docstring)."""
