@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--widths", default="F,76")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--rows", default="all", help="all, or P:p = rank p's 1/P nnz-balanced rows")
+    ap.add_argument("--attr", default=None,
+                    help="A/B a module attribute of sgc_amd.propagate (e.g. PAD_OVERLAP, "
+                         "COLUMN_GROUPS; values as ints) instead of a knob")
     ap.add_argument("--kwarg", default=None,
                     help="A/B a keyword of spmm() (threshold, hub_threshold) instead of a knob; "
                          "-1 = the default")
@@ -78,7 +81,10 @@ def main():
         outs = {}
 
         def select(v):
-            if args.kwarg:
+            if args.attr:
+                import importlib
+                setattr(importlib.import_module("sgc_amd.propagate"), args.attr, v)
+            elif args.kwarg:
                 cur["v"] = v
             else:
                 _lib.check(lib.sgc_set_tuning(args.knob.encode(), v), "set_tuning")
@@ -96,7 +102,8 @@ def main():
                 torch.cuda.synchronize()
                 ms[v].append(s.elapsed_time(e))
         same = all(torch.equal(outs[v], outs[values[0]]) for v in values)
-        rec = {"case": label, "knob": args.kwarg or args.knob, "bit_identical": bool(same)}
+        rec = {"case": label, "knob": args.attr or args.kwarg or args.knob,
+               "bit_identical": bool(same)}
         for v in values:
             rec[f"{v}_median_ms"] = round(float(np.median(ms[v])), 4)
             rec[f"{v}_min_ms"] = round(float(np.min(ms[v])), 4)
