@@ -714,7 +714,8 @@ def test_column_groups_tiny_cases_bit_exact(tiny_cases, G, monkeypatch):
 @pytest.mark.parametrize("F", [602, 304, 128, 256])
 def test_column_groups_medium_graph_bit_exact(oracle, F):
     """The default rule on a 4.2 M-nonzero graph (two groups at 128 and
-    > 256 floats, one at 129-256), forced 1, 3 and 4 groups, split hops (spmm over a row range) and
+    > 256 floats, one at 129-256), forced 1, 3 and 4 groups, X_0's re-layout
+    per group overlapped with hop 1 (PAD_OVERLAP) or in one copy, split hops (spmm over a row range) and
     the one-launch schedule: the oracle's bits."""
     from sgc_amd import graphs
     import importlib
@@ -729,14 +730,14 @@ def test_column_groups_medium_graph_bit_exact(oracle, F):
     csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=DEV)
     Xd = torch.from_numpy(X).to(DEV)
     assert column_groups_for(csr, F) == (1 if 128 < F <= 256 else 2)
-    saved = prop_mod.COLUMN_GROUPS
+    saved = prop_mod.COLUMN_GROUPS, prop_mod.PAD_OVERLAP
     try:
-        for G in (None, 1, 3, 4):
-            prop_mod.COLUMN_GROUPS = G
+        for G, overlap in ((None, False), (None, True), (1, False), (3, True), (4, False)):
+            prop_mod.COLUMN_GROUPS, prop_mod.PAD_OVERLAP = G, overlap
             out = propagate(csr, Xd, 2)
             part = spmm(csr, Xd, 1000, 37000)
             torch.cuda.synchronize()
-            assert bits_equal(out.cpu().numpy(), want2), (F, G)
+            assert bits_equal(out.cpu().numpy(), want2), (F, G, overlap)
             assert bits_equal(part.cpu().numpy(), want1[1000:37000]), (F, G)
     finally:
-        prop_mod.COLUMN_GROUPS = saved
+        prop_mod.COLUMN_GROUPS, prop_mod.PAD_OVERLAP = saved
