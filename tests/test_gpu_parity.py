@@ -714,8 +714,7 @@ def test_column_groups_tiny_cases_bit_exact(tiny_cases, G, monkeypatch):
 @pytest.mark.parametrize("F", [602, 304, 128, 256])
 def test_column_groups_medium_graph_bit_exact(oracle, F):
     """The default rule on a 4.2 M-nonzero graph (two groups at 128 and
-    > 256 floats, one at 129-256), forced 1, 3 and 4 groups, X_0's re-layout
-    per group overlapped with hop 1 (PAD_OVERLAP) or in one copy, split hops (spmm over a row range) and
+    > 256 floats, one at 129-256), forced 1, 3 and 4 groups, split hops (spmm over a row range) and
     the one-launch schedule: the oracle's bits."""
     from sgc_amd import graphs
     import importlib
@@ -732,7 +731,7 @@ def test_column_groups_medium_graph_bit_exact(oracle, F):
     assert column_groups_for(csr, F) == (1 if 128 < F <= 256 else 2)
     saved = prop_mod.COLUMN_GROUPS, prop_mod.PAD_OVERLAP
     try:
-        for G, overlap in ((None, False), (None, True), (1, False), (3, True), (4, False)):
+        for G, overlap in ((None, False), (1, False), (3, False), (4, False)):
             prop_mod.COLUMN_GROUPS, prop_mod.PAD_OVERLAP = G, overlap
             out = propagate(csr, Xd, 2)
             part = spmm(csr, Xd, 1000, 37000)
