@@ -33,8 +33,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--rows", default="all", help="all, or P:p = rank p's 1/P nnz-balanced rows")
     ap.add_argument("--attr", default=None,
-                    help="A/B a module attribute of sgc_amd.propagate (e.g. PAD_OVERLAP, "
-                         "COLUMN_GROUPS; values as ints) instead of a knob")
+                    help="A/B a module attribute of sgc_amd.propagate (e.g. COLUMN_GROUPS; "
+                         "values as ints) instead of a knob")
     ap.add_argument("--kwarg", default=None,
                     help="A/B a keyword of spmm() (threshold, hub_threshold) instead of a knob; "
                          "-1 = the default")

@@ -122,19 +122,6 @@ GROUPS_MIN_WIDTH = 128      # narrower launches gain nothing (76 floats: 0.77 vs
 GROUPS_WIDE_NNZ = 1 << 26   # from here four groups (RMAT shape)
 
 
-# Re-lay X_0's rows per column group, groups 1.. on a side stream under
-# hop 1's group-0 launch (propagate); off until measured (SGC_AMD_PAD_OVERLAP=1).
-PAD_OVERLAP = os.environ.get("SGC_AMD_PAD_OVERLAP", "0") != "0"
-_PAD_STREAMS = {}
-
-
-def _pad_side_stream(device):
-    s = _PAD_STREAMS.get(device)
-    if s is None:
-        s = _PAD_STREAMS[device] = torch.cuda.Stream(device=device)
-    return s
-
-
 def column_groups_for(csr, width):
     """Column groups for a plain launch of `width` features over `csr`."""
     if csr.device.type != "cuda" or not csr.cols_ascending or csr.nnz == 0:
@@ -647,31 +634,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
         bufs = [torch.empty((n, ldw), dtype=torch.float32, device=X.device)
                 for _ in range(n_bufs)]
         src, nxt = X, 0
-        waits = {}  # hop-1 group g -> event its X_0 rows are re-laid by
-        if pad and G > 1 and PAD_OVERLAP:
-            # group g of hop 1 gathers only the X_0 rows of its column range:
-            # re-lay range 0 in line, the others on a side stream under group
-            # 0's launch (row 0 -- what empty rows point their loads at -- is
-            # in range 0)
-            cuts = csr.group_cuts(G)
-            row_bytes = X.stride(0) * 4
-            _lib.check(lib.sgc_pad_rows_f32(_lib.ptr(X), X.stride(0), _lib.ptr(bufs[0]), ldw,
-                                            cuts[1], F, stream), "pad_rows_f32")
-            cur = torch.cuda.current_stream(X.device)
-            side = _pad_side_stream(X.device)
-            side.wait_stream(cur)
-            import ctypes
-            side_h = ctypes.c_void_p(side.cuda_stream)
-            for g in range(1, G):
-                r0, r1 = cuts[g], cuts[g + 1]
-                _lib.check(lib.sgc_pad_rows_f32(ctypes.c_void_p(X.data_ptr() + r0 * row_bytes),
-                                                X.stride(0),
-                                                ctypes.c_void_p(bufs[0].data_ptr() + r0 * ldw * 4),
-                                                ldw, r1 - r0, F, side_h), "pad_rows_f32")
-                waits[g] = torch.cuda.Event()
-                waits[g].record(side)
-            src, nxt = bufs[0][:, :F], 1 % len(bufs)
-        elif pad:
+        if pad:
             _lib.check(lib.sgc_pad_rows_f32(_lib.ptr(X), X.stride(0), _lib.ptr(bufs[0]), ldw, n, F,
                                             stream), "pad_rows_f32")
             src, nxt = bufs[0][:, :F], 1 % len(bufs)
@@ -682,9 +645,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                      (SPMM_Y_PADDED if dst is not out else 0) | x_flags(src))
             if hop_hook:
                 hop_hook("start", h)
-            for g, (c, cp, gflags) in enumerate(parts):  # column groups: 0 plain, 1.. accumulate
-                if h == 0 and g in waits:
-                    torch.cuda.current_stream(X.device).wait_event(waits[g])
+            for c, cp, gflags in parts:  # column groups: 0 plain, 1.. accumulate
                 _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(c.row_ptr), _lib.ptr(c.col_idx),
                                                    _lib.ptr(c.val), 0, n, _lib.ptr(src),
                                                    src.stride(0), _lib.ptr(dst), dst.stride(0),

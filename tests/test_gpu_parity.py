@@ -729,14 +729,14 @@ def test_column_groups_medium_graph_bit_exact(oracle, F):
     csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=DEV)
     Xd = torch.from_numpy(X).to(DEV)
     assert column_groups_for(csr, F) == (1 if 128 < F <= 256 else 2)
-    saved = prop_mod.COLUMN_GROUPS, prop_mod.PAD_OVERLAP
+    saved = prop_mod.COLUMN_GROUPS
     try:
-        for G, overlap in ((None, False), (1, False), (3, False), (4, False)):
-            prop_mod.COLUMN_GROUPS, prop_mod.PAD_OVERLAP = G, overlap
+        for G in (None, 1, 3, 4):
+            prop_mod.COLUMN_GROUPS = G
             out = propagate(csr, Xd, 2)
             part = spmm(csr, Xd, 1000, 37000)
             torch.cuda.synchronize()
-            assert bits_equal(out.cpu().numpy(), want2), (F, G, overlap)
+            assert bits_equal(out.cpu().numpy(), want2), (F, G)
             assert bits_equal(part.cpu().numpy(), want1[1000:37000]), (F, G)
     finally:
-        prop_mod.COLUMN_GROUPS, prop_mod.PAD_OVERLAP = saved
+        prop_mod.COLUMN_GROUPS = saved
