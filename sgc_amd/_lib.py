@@ -77,6 +77,7 @@ SIGNATURES = {
     "sgc_mgpu_propagate": (ctypes.c_int, [_i64, _p, _i64, _p, _i64, _i64, _i32, _p]),
     "sgc_mgpu_detach": (ctypes.c_int, [_i64]),
     "sgc_mgpu_finalize": (ctypes.c_int, []),
+    "sgc_warmup": (ctypes.c_int, [_u32, _p]),
 }
 
 ABI_VERSION = 1

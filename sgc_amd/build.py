@@ -13,7 +13,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsgc_amd.so")
 SOURCES = ["capi.hip", "spmm.hip", "ingest.hip", "linear.hip", "normalize.hip", "xent.hip",
-           "subgraph.hip", "cpu.hip", "mgpu.hip", "plan.hip", "groups.hip"]
+           "subgraph.hip", "cpu.hip", "mgpu.hip", "plan.hip", "groups.hip", "sort.hip"]
 
 
 def _headers():

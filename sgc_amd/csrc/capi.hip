@@ -298,6 +298,28 @@ int sgc_linear_xent_f32(const float *X, int64_t ldx, const float *W, const float
                            workspace_bytes, as_stream(stream));
 }
 
+int sgc_warmup(uint32_t units, void *stream) {
+    SGC_REQUIRE((units & ~7u) == 0, SGC_EINVAL, "warmup: unknown unit bits 0x%x", units);
+    hipStream_t s = as_stream(stream);
+    if (units & SGC_WARM_PROPAGATE) {
+        SGC_HIP_CHECK(warm_spmm(s));
+        SGC_HIP_CHECK(warm_ingest(s));
+        SGC_HIP_CHECK(warm_plan(s));
+        SGC_HIP_CHECK(warm_sort(s));
+        SGC_HIP_CHECK(warm_groups(s));
+    }
+    if (units & SGC_WARM_CLASSIFIER) {
+        SGC_HIP_CHECK(warm_linear(s));
+        SGC_HIP_CHECK(warm_xent(s));
+    }
+    if (units & SGC_WARM_LOADERS) {
+        SGC_HIP_CHECK(warm_normalize(s));
+        SGC_HIP_CHECK(warm_subgraph(s));
+    }
+    SGC_HIP_CHECK(hipStreamSynchronize(s));
+    return SGC_OK;
+}
+
 int sgc_timing_enable(int on) { return timing_enable(on); }
 
 int sgc_timing_collect(float *light_ms_host, float *hub_ms_host, int64_t capacity,

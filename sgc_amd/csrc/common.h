@@ -31,6 +31,28 @@ void set_error(const char *fmt, ...);
 
 static constexpr int kWave = 64;  // CDNA wavefront width (never 32)
 
+// Code-object warm-up (sgc_warmup): the runtime loads a translation unit's
+// code object on the first launch of any of its kernels, so one empty launch
+// per unit moves that load out of the first real call.  SGC_WARM_UNIT(name)
+// defines `hipError_t name(hipStream_t)` launching this unit's empty kernel.
+#define SGC_WARM_UNIT(name)                                                 \
+    namespace {                                                             \
+    __global__ void name##_kernel() {}                                      \
+    }                                                                       \
+    hipError_t name(hipStream_t s) {                                        \
+        hipLaunchKernelGGL(name##_kernel, dim3(1), dim3(kWave), 0, s);      \
+        return hipGetLastError();                                           \
+    }
+hipError_t warm_spmm(hipStream_t);
+hipError_t warm_ingest(hipStream_t);
+hipError_t warm_plan(hipStream_t);
+hipError_t warm_sort(hipStream_t);
+hipError_t warm_groups(hipStream_t);
+hipError_t warm_linear(hipStream_t);
+hipError_t warm_xent(hipStream_t);
+hipError_t warm_normalize(hipStream_t);
+hipError_t warm_subgraph(hipStream_t);
+
 inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 // V consecutive fp32 in one lane: float / float2 / float4 register vectors,

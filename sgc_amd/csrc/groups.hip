@@ -205,4 +205,6 @@ int colsplit(const int32_t *row_ptr, const int32_t *col_idx, const float *val, i
     return SGC_OK;
 }
 
+SGC_WARM_UNIT(warm_groups)
+
 }  // namespace sgc

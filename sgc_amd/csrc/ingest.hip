@@ -11,10 +11,9 @@
 // Fast path (the reference's own S is lexsorted): one streaming pass checks
 // ranges and sortedness and narrows col/val into place; a second pass writes
 // row_ptr from the row transitions.  Unsorted input: stable LSD radix sort
-// (hipCUB) of (row, position) pairs, then a gather.
+// (the library's own, sort.hip) of (row, position) pairs, then a gather.
 #include "common.h"
-
-#include <hipcub/hipcub.hpp>
+#include "sort.h"
 
 namespace sgc {
 
@@ -65,10 +64,10 @@ __global__ void row_ptr_from_sorted_kernel(const IdxT *__restrict__ rows, int64_
 }
 
 __global__ void narrow_rows_iota_kernel(const int64_t *__restrict__ rows, int64_t nnz,
-                                        int32_t *__restrict__ keys, int32_t *__restrict__ pos) {
+                                        uint32_t *__restrict__ keys, int32_t *__restrict__ pos) {
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < nnz;
          k += (int64_t)gridDim.x * blockDim.x) {
-        keys[k] = (int32_t)rows[k];
+        keys[k] = (uint32_t)rows[k];
         pos[k] = (int32_t)k;
     }
 }
@@ -132,26 +131,17 @@ struct Carve {
     }
 };
 
-size_t radix_temp_bytes(int64_t nnz, int64_t n_rows) {
-    size_t bytes = 0;
-    int end_bit = 1;
-    while (end_bit < 31 && (int64_t(1) << end_bit) < n_rows) ++end_bit;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t *)nullptr, (int32_t *)nullptr,
-                                       (const int32_t *)nullptr, (int32_t *)nullptr, (int)nnz, 0,
-                                       end_bit);
-    return bytes;
-}
-
 size_t workspace_layout(int64_t n_rows, int64_t nnz, char *base, uint32_t **flags,
-                        int32_t **keys_in, int32_t **keys_out, int32_t **pos_in,
+                        uint32_t **keys_in, uint32_t **keys_out, int32_t **pos_in,
                         int32_t **pos_out, void **temp, size_t *temp_bytes) {
+    (void)n_rows;
     Carve cv{base};
     *flags = cv.take<uint32_t>(1);
-    *keys_in = cv.take<int32_t>(nnz);
-    *keys_out = cv.take<int32_t>(nnz);
+    *keys_in = cv.take<uint32_t>(nnz);
+    *keys_out = cv.take<uint32_t>(nnz);
     *pos_in = cv.take<int32_t>(nnz);
     *pos_out = cv.take<int32_t>(nnz);
-    *temp_bytes = radix_temp_bytes(nnz, n_rows);
+    *temp_bytes = (size_t)radix_sort_workspace(nnz);
     *temp = cv.take<char>(*temp_bytes);
     return cv.used + 256;
 }
@@ -162,8 +152,8 @@ int coo_to_csr_workspace(int64_t n_rows, int64_t nnz, size_t *bytes) {
     SGC_REQUIRE(bytes, SGC_EINVAL, "coo_to_csr_workspace: null");
     SGC_REQUIRE(n_rows >= 0 && nnz >= 0 && n_rows < INT32_MAX && nnz < INT32_MAX, SGC_ERANGE,
                 "coo_to_csr: n_rows/nnz beyond int32 CSR");
-    uint32_t *f;
-    int32_t *a, *b, *c, *d;
+    uint32_t *f, *a, *b;
+    int32_t *c, *d;
     void *t;
     size_t tb;
     *bytes = workspace_layout(n_rows, nnz, nullptr, &f, &a, &b, &c, &d, &t, &tb);
@@ -180,8 +170,8 @@ int coo_to_csr(const int64_t *rows, const int64_t *cols, const float *vals, int6
     SGC_REQUIRE(row_ptr && ws, SGC_EINVAL, "coo_to_csr: null pointer");
     SGC_REQUIRE(nnz == 0 || (rows && cols && vals && col_idx && val_out), SGC_EINVAL,
                 "coo_to_csr: null pointer");
-    uint32_t *flags;
-    int32_t *keys_in, *keys_out, *pos_in, *pos_out;
+    uint32_t *flags, *keys_in, *keys_out;
+    int32_t *pos_in, *pos_out;
     void *temp;
     size_t temp_bytes;
     const size_t need = workspace_layout(n_rows, nnz, (char *)ws, &flags, &keys_in, &keys_out,
@@ -209,18 +199,17 @@ int coo_to_csr(const int64_t *rows, const int64_t *cols, const float *vals, int6
                            0, stream, rows, nnz, n_rows, row_ptr);
         SGC_HIP_CHECK(hipGetLastError());
     } else {
-        int end_bit = 1;
-        while (end_bit < 31 && (int64_t(1) << end_bit) < n_rows) ++end_bit;
         hipLaunchKernelGGL(narrow_rows_iota_kernel, dim3(grid_for(nnz)), dim3(kBlock), 0, stream,
                            rows, nnz, keys_in, pos_in);
         SGC_HIP_CHECK(hipGetLastError());
-        size_t tb = temp_bytes;
-        SGC_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp, tb, keys_in, keys_out, pos_in,
-                                                         pos_out, (int)nnz, 0, end_bit, stream));
+        const int rc = radix_sort_pairs(keys_in, pos_in, keys_out, pos_out, nnz,
+                                        (uint32_t)std::max<int64_t>(0, n_rows - 1), false, temp,
+                                        (int64_t)temp_bytes, stream);
+        if (rc != SGC_OK) return rc;
         hipLaunchKernelGGL(gather_kernel, dim3(grid_for(nnz)), dim3(kBlock), 0, stream, pos_out,
                            cols, vals, nnz, col_idx, val_out);
         SGC_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(row_ptr_from_sorted_kernel<int32_t>, dim3(grid_for(nnz + 1)),
+        hipLaunchKernelGGL(row_ptr_from_sorted_kernel<uint32_t>, dim3(grid_for(nnz + 1)),
                            dim3(kBlock), 0, stream, keys_out, nnz, n_rows, row_ptr);
         SGC_HIP_CHECK(hipGetLastError());
         hipLaunchKernelGGL(csr_cols_ascending_kernel, dim3(grid_for(n_rows)), dim3(kBlock), 0,
@@ -264,5 +253,7 @@ int csr64_to_csr(const int64_t *crow, const int64_t *col, const float *vals, int
     SGC_REQUIRE(!(f & kOutOfRange), SGC_ERANGE, "csr64_to_csr: index out of range");
     return SGC_OK;
 }
+
+SGC_WARM_UNIT(warm_ingest)
 
 }  // namespace sgc

@@ -102,4 +102,6 @@ int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *
     return SGC_OK;
 }
 
+SGC_WARM_UNIT(warm_linear)
+
 }  // namespace sgc

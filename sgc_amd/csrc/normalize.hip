@@ -291,4 +291,6 @@ int csr_to_coo64(const int32_t *row_ptr, const int32_t *col, int64_t n, int64_t 
     return SGC_OK;
 }
 
+SGC_WARM_UNIT(warm_normalize)
+
 }  // namespace sgc

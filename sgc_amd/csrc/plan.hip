@@ -7,23 +7,25 @@
 // light rows longest first; SGC_SPMM_LIGHT_ORDER), without their host sorts,
 // their row_ptr read-back and three of their four synchronisations.
 // A schedule only: results never depend on it.
-#include <hipcub/hipcub.hpp>
-
+// The sort is the library's own (sort.hip, 11-bit digits: two passes up to
+// degree 4,194,303): hipCUB's made this translation unit's code object
+// 2.2 MB, whose load cost the first plan of a process 12-46 ms.
 #include "common.h"
+#include "sort.h"
 
 namespace sgc {
 
 namespace {
 
 __global__ void plan_keys_kernel(const int32_t *__restrict__ row_ptr, int row_begin, int n_rows,
-                                 int threshold, int hub_threshold, int32_t *__restrict__ deg,
+                                 int threshold, int hub_threshold, uint32_t *__restrict__ deg,
                                  int32_t *__restrict__ ids, int32_t *__restrict__ counts) {
     int heavy = 0, hub = 0, top = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_rows;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int row = row_begin + (int)i;
         const int d = row_ptr[row + 1] - row_ptr[row];
-        deg[i] = d;
+        deg[i] = (uint32_t)d;
         ids[i] = row;
         heavy += d > threshold;
         hub += d > hub_threshold;
@@ -42,13 +44,7 @@ __global__ void plan_keys_kernel(const int32_t *__restrict__ row_ptr, int row_be
     }
 }
 
-size_t sort_temp_bytes(int64_t n) {
-    size_t bytes = 0;
-    (void)hipcub::DeviceRadixSort::SortPairsDescending(
-        nullptr, bytes, (const int32_t *)nullptr, (int32_t *)nullptr, (const int32_t *)nullptr,
-        (int32_t *)nullptr, (int)n, 0, 32);
-    return bytes;
-}
+size_t sort_temp_bytes(int64_t n) { return (size_t)radix_sort_workspace(n); }
 
 constexpr size_t kAlign = 256;
 size_t up(size_t b) { return (b + kAlign - 1) / kAlign * kAlign; }
@@ -78,9 +74,9 @@ int plan_sorted(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int3
     char *w = static_cast<char *>(workspace);
     int32_t *counts = reinterpret_cast<int32_t *>(w);
     w += up(3 * sizeof(int32_t));
-    int32_t *deg = reinterpret_cast<int32_t *>(w);
+    uint32_t *deg = reinterpret_cast<uint32_t *>(w);
     w += up((size_t)n * sizeof(int32_t));
-    int32_t *deg_sorted = reinterpret_cast<int32_t *>(w);
+    uint32_t *deg_sorted = reinterpret_cast<uint32_t *>(w);
     w += up((size_t)n * sizeof(int32_t));
     int32_t *ids = reinterpret_cast<int32_t *>(w);
     w += up((size_t)n * sizeof(int32_t));
@@ -90,16 +86,19 @@ int plan_sorted(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int3
     hipLaunchKernelGGL(plan_keys_kernel, dim3(blocks), dim3(256), 0, stream, row_ptr,
                        (int)row_begin, (int)n, threshold, hub_threshold, deg, ids, counts);
     SGC_HIP_CHECK(hipGetLastError());
-    // stable: equal degrees keep ascending row order
-    SGC_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(w, temp, deg, deg_sorted, ids, plan,
-                                                               (int)n, 0, 32, stream));
     int32_t c[3] = {0, 0, 0};
     SGC_HIP_CHECK(hipMemcpyAsync(c, counts, sizeof(c), hipMemcpyDeviceToHost, stream));
     SGC_HIP_CHECK(hipStreamSynchronize(stream));
     counts_host[0] = c[0];
     counts_host[1] = c[1];
     counts_host[2] = c[2];
-    return SGC_OK;
+    // stable: equal degrees keep ascending row order; the longest row (read
+    // back above) sets the passes.  Enqueued after the read-back: the plan
+    // is ready in stream order.
+    return radix_sort_pairs(deg, ids, deg_sorted, plan, n, (uint32_t)std::max(0, c[2]), true, w,
+                            (int64_t)temp, stream);
 }
+
+SGC_WARM_UNIT(warm_plan)
 
 }  // namespace sgc

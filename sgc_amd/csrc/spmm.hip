@@ -565,14 +565,16 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
         // clamped to its last one; a row without nonzeros reads X row 0 (its
         // FMAs are all skipped)
         const bool stager = sub < R && l < LB;
+        // Never predicated: a conditional load makes (c, v) a phi whose
+        // default copy must wait for every load in flight (s_waitcnt
+        // vmcnt(0) once per block: the gathers of the steps ahead drained
+        // at every LB nonzeros).  Lanes without a nonzero to stage read
+        // nonzero 0 (valid: n_max > 0 means the CSR has one); the value is
+        // either not staged or belongs to a row whose FMAs are all skipped.
         auto fetch = [&](int base, int &c, float &v) {
-            c = 0;
-            v = 0.0f;
-            if (len > 0 && l < LB) {
-                const int kk = k0 + min(base + l, len - 1);
-                c = col[kk];
-                v = val[kk];
-            }
+            const int kk = (len > 0 && l < LB) ? k0 + min(base + l, len - 1) : 0;
+            c = col[kk];
+            v = val[kk];
         };
         auto stage = [&](int buf, int c, float v) {
             if (stager) {
@@ -1706,5 +1708,7 @@ int light_order(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int3
     *n_light_host = n_light;
     return SGC_OK;
 }
+
+SGC_WARM_UNIT(warm_spmm)
 
 }  // namespace sgc

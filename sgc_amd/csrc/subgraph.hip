@@ -226,4 +226,6 @@ int subgraph_fill(const int32_t *row_ptr, const int32_t *col, const double *val,
     return SGC_OK;
 }
 
+SGC_WARM_UNIT(warm_subgraph)
+
 }  // namespace sgc

@@ -383,4 +383,6 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
     return SGC_OK;
 }
 
+SGC_WARM_UNIT(warm_xent)
+
 }  // namespace sgc

@@ -704,6 +704,30 @@ class GraphedPropagation:
         return self.out
 
 
+WARM_PROPAGATE, WARM_CLASSIFIER, WARM_LOADERS = 1, 2, 4  # sgc_warmup units (sgc_amd.h)
+_warmed = {}
+
+
+def warmup(device=None, units=WARM_PROPAGATE | WARM_CLASSIFIER):
+    """Load the library's code objects on `device` now (sgc_warmup: one empty
+    launch per translation unit), once per process and device, so that the
+    first sgc_precompute a caller times (reddit.py:43,72-74) does not pay
+    them.  The loaders call it when they move data to the GPU.  Returns the
+    seconds it took (0.0 when already done)."""
+    import time
+    d = torch.device("cuda") if device is None else torch.device(device)
+    dev = torch.device("cuda", d.index if d.index is not None else torch.cuda.current_device())
+    key = (dev.index, int(units))
+    if key in _warmed:
+        return 0.0
+    lib = _lib.load()
+    t = time.perf_counter()
+    with torch.cuda.device(dev):
+        _lib.check(lib.sgc_warmup(int(units), _lib.stream_handle(dev)), "warmup")
+    _warmed[key] = time.perf_counter() - t
+    return _warmed[key]
+
+
 def kernel_timing(on: bool):
     """Turn per-kernel launch timing on/off (sgc_timing_enable; diagnostics)."""
     _lib.check(_lib.load().sgc_timing_enable(1 if on else 0), "timing_enable")

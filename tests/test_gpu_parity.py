@@ -649,6 +649,60 @@ def test_plan_sorted_matches_host_plan(r0, r1, th, hub):
     assert np.array_equal(out[:n].cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("n,top", [(20000, 50000), (9000, 5_000_000), (3000, 2047), (2049, 2048),
+                                   (70000, 0)])
+def test_plan_sorted_multipass(n, top):
+    """The plan's radix sort (sort.hip) over several tiles and 1-3 digit
+    passes: power-law degrees up to `top` (2,047 and 2,048 sit either side
+    of one 11-bit digit; top 0 = every row empty), longest first, ties in row
+    order, as a stable host sort."""
+    import ctypes
+    from sgc_amd import _lib
+    rng = np.random.default_rng(n + top)
+    deg = np.minimum(rng.pareto(1.2, n) * 3, top).astype(np.int64)
+    if top:
+        deg[rng.integers(0, n, 3)] = top  # ties at the top
+    rp = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    assert rp[-1] < 2**31
+    rp_d = torch.from_numpy(rp.astype(np.int32)).to(DEV)
+    lib = _lib.load()
+    out = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    wb = lib.sgc_plan_sorted_workspace(n)
+    ws = torch.empty(max(1, wb), dtype=torch.uint8, device=DEV)
+    counts = (ctypes.c_int64 * 3)()
+    _lib.check(lib.sgc_plan_sorted(_lib.ptr(rp_d), 0, n, 64, 1024, _lib.ptr(out), _lib.ptr(ws), wb,
+                                   ctypes.cast(counts, ctypes.c_void_p), _lib.stream_handle(DEV)),
+               "plan_sorted")
+    want = np.argsort(-deg, kind="stable").astype(np.int32)
+    assert list(counts) == [int((deg > 64).sum()), int((deg > 1024).sum()), int(deg.max())]
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("n", [3000, 300000])
+def test_ingest_unsorted_multipass(n, oracle):
+    """Row-unsorted COO with duplicates over n rows (one or two 11-bit digit
+    passes of the ingest's radix sort, many tiles): the CSR is the oracle's
+    stable counting sort, bit for bit, and so is one hop."""
+    from sgc_amd.propagate import STATUS_ROWS_SORTED, DeviceCSR, spmm
+    rng = np.random.default_rng(n)
+    nnz = 8 * n
+    rows = rng.integers(0, n, nnz)
+    cols = rng.integers(0, n, nnz)
+    rows[: nnz // 8] = rows[0]  # a hub row with duplicates
+    vals = rng.standard_normal(nnz).astype(np.float32)
+    idx = torch.from_numpy(np.stack([rows, cols]).astype(np.int64))
+    adj = torch.sparse_coo_tensor(idx, torch.from_numpy(vals), (n, n)).to(DEV)
+    csr = DeviceCSR.from_torch(adj)
+    assert not csr.status & STATUS_ROWS_SORTED
+    rp, ci, va = oracle.coo_to_csr(n, n, rows, cols, vals)
+    assert np.array_equal(csr.row_ptr.cpu().numpy(), rp)
+    assert np.array_equal(csr.col_idx.cpu().numpy(), ci)
+    assert bits_equal(csr.val.cpu().numpy(), va)
+    X = rng.standard_normal((n, 5)).astype(np.float32)
+    y = spmm(csr, torch.from_numpy(X).to(DEV))
+    assert bits_equal(y.cpu().numpy(), oracle.spmm_csr(rp, ci, va, X, 0, n))
+
+
 # ---------------------------------------------------------------------------
 # Column groups: one hop as G launches over column ranges (accumulating).
 
