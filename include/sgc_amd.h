@@ -272,6 +272,25 @@ int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const floa
                       int32_t heavy_threshold, void *workspace, int64_t workspace_bytes,
                       void *stream);
 
+/* The same loop over S split into `groups` column groups (sgc_csr_colsplit:
+ * row_ptrs [groups][n_rows+1] absolute into one col_idx / val pair; rows with
+ * ascending columns), each hop as `groups` launches -- group 0 plain, groups
+ * 1.. with SGC_SPMM_ACCUMULATE -- which is bit-identical to one launch per
+ * hop and faster at Reddit shape.  Per group g:
+ * plans_host[g] / n_heavy_host[g] / n_hub_host[g] / thresholds_host[g] =
+ * sgc_plan_sorted over group g's CSR (plans_host NULL = no plans), and
+ * plan_flags_host[g] (may be NULL) = SGC_SPMM_LIGHT_ORDER (plans_host[g]
+ * lists every row, as sgc_plan_sorted writes it) | SGC_SPMM_HUB_SERIAL.
+ * groups = 1 with row_ptrs = the CSR's row_ptr is sgc_propagate_f32 with
+ * plan flags.  Same workspace as sgc_propagate_f32. */
+int sgc_propagate_groups_f32(int32_t groups, const int32_t *row_ptrs, const int32_t *col_idx,
+                             const float *val, int64_t n_rows, const float *X0, int64_t ldx,
+                             float *out, int64_t ldo, int64_t F, int32_t K,
+                             const int32_t *const *plans_host, const int64_t *n_heavy_host,
+                             const int64_t *n_hub_host, const int32_t *thresholds_host,
+                             const uint32_t *plan_flags_host, void *workspace,
+                             int64_t workspace_bytes, void *stream);
+
 /* Row-strided copy dst[i, 0:F] = src[i, 0:F] (re-layout of feature rows). */
 int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd,
                      int64_t n_rows, int64_t F, void *stream);
@@ -287,6 +306,19 @@ int64_t sgc_aligned_ld(int64_t F);
  * ------------------------------------------------------------------------- */
 int sgc_linear_f32(const float *X, int64_t ldx, const float *W, const float *b,
                    float *Y, int64_t ldy, int64_t M, int64_t K, int64_t C, void *stream);
+
+/* Backward of sgc_linear_f32 for the weights (what autograd runs for
+ * nn.Linear after F.cross_entropy(model(x), y).backward() in the closures of
+ * citation.py:47-49 and reddit.py:55-58):  dW[C,K] = dY^T X,  db[C] = sum_m dY
+ * (db may be NULL), from one read of X on fp32 MFMA; dY [M,C] with row stride
+ * ldd.  C <= 64.  Fixed-order reductions: bitwise reproducible run to run,
+ * within fp32 tolerance of torch.  workspace: sgc_linear_backward_workspace
+ * (M, K, C) bytes.  (dX = dY W, needed only when x requires a gradient, is
+ * not computed here.) */
+int64_t sgc_linear_backward_workspace(int64_t M, int64_t K, int64_t C);
+int sgc_linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ldd,
+                            int64_t M, int64_t K, int64_t C, float *dW, float *db,
+                            void *workspace, int64_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Fused classifier training step: for the SGC closure
@@ -346,9 +378,10 @@ int sgc_propagate_f32_cpu(const int32_t *row_ptr, const int32_t *col_idx, const 
  * heaviest first followed by the light rows in SGC_SPMM_LIGHT_ORDER order,
  * exactly what sgc_plan_build + sgc_plan_light_order write together.
  * counts_host[0] = rows above threshold (n_heavy), [1] = rows above
- * hub_threshold (n_hub), [2] = the longest row's nonzeros.  One stream
- * synchronisation (the counts); workspace of sgc_plan_sorted_workspace(n)
- * bytes on the device.  Replaces nothing in the reference (a schedule). */
+ * hub_threshold (n_hub), [2] = the longest row's nonzeros.  Synchronous (two
+ * stream synchronisations: the counts, then the sort); workspace of
+ * sgc_plan_sorted_workspace(n) bytes on the device.  Replaces nothing in the
+ * reference (a schedule). */
 int64_t sgc_plan_sorted_workspace(int64_t n_rows);
 int sgc_plan_sorted(const int32_t *row_ptr, int64_t row_begin, int64_t row_end,
                     int32_t threshold, int32_t hub_threshold, int32_t *plan, void *workspace,

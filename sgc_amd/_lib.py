@@ -49,6 +49,8 @@ SIGNATURES = {
     "sgc_propagate_workspace": (_i64, [_i64, _i64, _i64, _i32]),
     "sgc_propagate_f32": (ctypes.c_int, [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i64, _i32,
                                          _p, _i64, _i64, _i32, _p, _i64, _p]),
+    "sgc_propagate_groups_f32": (ctypes.c_int, [_i32, _p, _p, _p, _i64, _p, _i64, _p, _i64, _i64,
+                                                 _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "sgc_pad_rows_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i64, _p]),
     "sgc_aligned_ld": (_i64, [_i64]),
     "sgc_linear_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
@@ -78,6 +80,9 @@ SIGNATURES = {
     "sgc_mgpu_detach": (ctypes.c_int, [_i64]),
     "sgc_mgpu_finalize": (ctypes.c_int, []),
     "sgc_warmup": (ctypes.c_int, [_u32, _p]),
+    "sgc_linear_backward_workspace": (_i64, [_i64, _i64, _i64]),
+    "sgc_linear_backward_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i64, _i64, _p, _p, _p,
+                                               _i64, _p]),
 }
 
 ABI_VERSION = 1

@@ -48,6 +48,10 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
                     const int64_t *labels, int64_t M, int64_t K, int64_t C, float *loss,
                     float *dW, float *db, float *logits, int64_t ldl, void *ws, int64_t ws_bytes,
                     hipStream_t s);
+int64_t linear_backward_workspace_bytes(int64_t M, int64_t K, int64_t C);
+int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ldd, int64_t M,
+                        int64_t K, int64_t C, float *dW, float *db, void *ws, int64_t ws_bytes,
+                        hipStream_t s);
 int64_t subgraph_workspace(int64_t n, int64_t m, int64_t nnz);
 int subgraph_count(const int32_t *row_ptr, const int32_t *col, int64_t n, const int64_t *idx,
                    int64_t m, int64_t nnz, int32_t *out_row_ptr, void *ws, int64_t ws_bytes,
@@ -232,15 +236,25 @@ int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int
     return launch_pad_rows(src, lds, dst, ldd, n_rows, F, as_stream(stream));
 }
 
-int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
-                      int64_t n_rows, const float *X0, int64_t ldx, float *out, int64_t ldo,
-                      int64_t F, int32_t K, const int32_t *plan, int64_t n_heavy, int64_t n_hub,
-                      int32_t heavy_threshold, void *workspace, int64_t workspace_bytes,
-                      void *stream) {
+int sgc_propagate_groups_f32(int32_t groups, const int32_t *row_ptrs, const int32_t *col_idx,
+                             const float *val, int64_t n_rows, const float *X0, int64_t ldx,
+                             float *out, int64_t ldo, int64_t F, int32_t K,
+                             const int32_t *const *plans_host, const int64_t *n_heavy_host,
+                             const int64_t *n_hub_host, const int32_t *thresholds_host,
+                             const uint32_t *plan_flags_host, void *workspace,
+                             int64_t workspace_bytes, void *stream) {
     hipStream_t s = as_stream(stream);
     SGC_REQUIRE(K >= 0, SGC_EINVAL, "propagate: negative degree %d", K);
-    SGC_REQUIRE(X0 && out, SGC_EINVAL, "propagate: null pointer");
+    SGC_REQUIRE(groups >= 1 && groups <= 8, SGC_EINVAL, "propagate: groups must be 1..8");
+    SGC_REQUIRE(X0 && out && row_ptrs, SGC_EINVAL, "propagate: null pointer");
     SGC_REQUIRE(ldx >= F && ldo >= F && F >= 0 && n_rows >= 0, SGC_EINVAL, "propagate: bad shape");
+    SGC_REQUIRE(!plans_host || (n_heavy_host && n_hub_host && thresholds_host), SGC_EINVAL,
+                "propagate: plans without their counts");
+    constexpr uint32_t kPlanFlags = SGC_SPMM_LIGHT_ORDER | SGC_SPMM_HUB_SERIAL;
+    if (plan_flags_host)
+        for (int g = 0; g < groups; ++g)
+            SGC_REQUIRE((plan_flags_host[g] & ~kPlanFlags) == 0, SGC_EINVAL,
+                        "propagate: plan flags may only be LIGHT_ORDER / HUB_SERIAL");
     if (K == 0)
         return sgc_pad_rows_f32(X0, ldx, out, ldo, n_rows, F, stream);
     if (n_rows == 0 || F == 0) return SGC_OK;
@@ -271,9 +285,17 @@ int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const floa
         const uint32_t fl = (src != X0 ? SGC_SPMM_X_PADDED : 0u) | (last ? 0u : SGC_SPMM_Y_PADDED) |
                             (n_rows < (int64_t(1) << 24) && n_rows * lds * 4 < (int64_t(1) << 32)
                                  ? SGC_SPMM_X_UNDER_4G : 0u);
-        const int rc = launch_spmm(row_ptr, col_idx, val, 0, n_rows, src, lds, dst, ldd, F, plan,
-                                   plan ? n_heavy : 0, plan ? n_hub : 0, heavy_threshold, fl, s);
-        if (rc) return rc;
+        // column groups: group 0 plain, groups 1.. continue its chains
+        for (int g = 0; g < groups; ++g) {
+            const int32_t *plan = plans_host ? plans_host[g] : nullptr;
+            const uint32_t gf = fl | (g ? (uint32_t)SGC_SPMM_ACCUMULATE : 0u) |
+                                (plan && plan_flags_host ? plan_flags_host[g] : 0u);
+            const int rc = launch_spmm(row_ptrs + (int64_t)g * (n_rows + 1), col_idx, val, 0,
+                                       n_rows, src, lds, dst, ldd, F, plan,
+                                       plan ? n_heavy_host[g] : 0, plan ? n_hub_host[g] : 0,
+                                       plan ? thresholds_host[g] : 0, gf, s);
+            if (rc) return rc;
+        }
         src = dst;
         lds = ldd;
         next ^= 1;
@@ -281,9 +303,31 @@ int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const floa
     return SGC_OK;
 }
 
+int sgc_propagate_f32(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
+                      int64_t n_rows, const float *X0, int64_t ldx, float *out, int64_t ldo,
+                      int64_t F, int32_t K, const int32_t *plan, int64_t n_heavy, int64_t n_hub,
+                      int32_t heavy_threshold, void *workspace, int64_t workspace_bytes,
+                      void *stream) {
+    const int32_t *plans[1] = {plan};
+    return sgc_propagate_groups_f32(1, row_ptr, col_idx, val, n_rows, X0, ldx, out, ldo, F, K,
+                                    plan ? plans : nullptr, &n_heavy, &n_hub, &heavy_threshold,
+                                    nullptr, workspace, workspace_bytes, stream);
+}
+
 int sgc_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                    int64_t ldy, int64_t M, int64_t K, int64_t C, void *stream) {
     return launch_linear_f32(X, ldx, W, b, Y, ldy, M, K, C, as_stream(stream));
+}
+
+int64_t sgc_linear_backward_workspace(int64_t M, int64_t K, int64_t C) {
+    return linear_backward_workspace_bytes(M, K, C);
+}
+
+int sgc_linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ldd, int64_t M,
+                            int64_t K, int64_t C, float *dW, float *db, void *workspace,
+                            int64_t workspace_bytes, void *stream) {
+    return linear_backward_f32(X, ldx, dY, ldd, M, K, C, dW, db, workspace, workspace_bytes,
+                               as_stream(stream));
 }
 
 int64_t sgc_linear_xent_workspace(int64_t M, int64_t K, int64_t C) {

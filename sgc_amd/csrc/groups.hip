@@ -19,6 +19,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace sgc {
 
@@ -203,6 +204,58 @@ int colsplit(const int32_t *row_ptr, const int32_t *col_idx, const float *val, i
                        col_idx, val, n, (int)groups, cuts, row_ptrs, col_out, val_out);
     SGC_HIP_CHECK(hipGetLastError());
     return SGC_OK;
+}
+
+// Every row's columns strictly ascending?  (the ingest's status bit 2 for a
+// CSR the caller built itself; column groups need it).  Synchronous.
+__global__ void cols_ascending_kernel(const int32_t *__restrict__ row_ptr,
+                                      const int32_t *__restrict__ col, int64_t n,
+                                      int32_t *__restrict__ bad) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        for (int32_t k = row_ptr[i] + 1; k < row_ptr[i + 1]; ++k)
+            if (col[k - 1] >= col[k]) {
+                atomicOr(bad, 1);
+                break;
+            }
+    }
+}
+
+int csr_cols_ascending(const int32_t *row_ptr, const int32_t *col_idx, int64_t n_rows,
+                       hipStream_t stream, bool *ascending) {
+    SGC_REQUIRE(row_ptr && ascending, SGC_EINVAL, "cols_ascending: null pointer");
+    *ascending = true;
+    if (n_rows <= 0) return SGC_OK;
+    int32_t *bad = nullptr;
+    SGC_HIP_CHECK(hipMallocAsync((void **)&bad, sizeof(int32_t), stream));
+    SGC_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int32_t), stream));
+    const int blocks = (int)std::min<int64_t>((n_rows + 255) / 256, 4096);
+    hipLaunchKernelGGL(cols_ascending_kernel, dim3(blocks), dim3(256), 0, stream, row_ptr,
+                       col_idx, n_rows, bad);
+    SGC_HIP_CHECK(hipGetLastError());
+    int32_t h = 0;
+    SGC_HIP_CHECK(hipMemcpyAsync(&h, bad, sizeof(h), hipMemcpyDeviceToHost, stream));
+    SGC_HIP_CHECK(hipFreeAsync(bad, stream));
+    SGC_HIP_CHECK(hipStreamSynchronize(stream));
+    *ascending = h == 0;
+    return SGC_OK;
+}
+
+// The size rule of sgc_amd/propagate.py column_groups_for (measured,
+// DESIGN.md 4.2): G = 1 below 4 M nonzeros, under 128 features or at 129-256
+// (the one-row kernel's single slice); 4 from 64 M nonzeros; else 2.
+// SGC_AMD_COLUMN_GROUPS=G forces G, as in the Python layer.
+int column_groups_rule(int64_t nnz, int64_t width) {
+    static const int forced = [] {
+        const char *e = getenv("SGC_AMD_COLUMN_GROUPS");
+        return e && *e ? atoi(e) : 0;
+    }();
+    if (nnz <= 0) return 1;
+    if (forced > 0) return std::min(forced, kGroupsMax);
+    if (width < 128 || nnz < (int64_t(1) << 22)) return 1;
+    if (nnz >= (int64_t(1) << 26)) return 4;
+    if (width > 128 && width <= 256) return 1;
+    return 2;
 }
 
 SGC_WARM_UNIT(warm_groups)

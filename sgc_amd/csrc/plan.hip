@@ -93,10 +93,13 @@ int plan_sorted(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int3
     counts_host[1] = c[1];
     counts_host[2] = c[2];
     // stable: equal degrees keep ascending row order; the longest row (read
-    // back above) sets the passes.  Enqueued after the read-back: the plan
-    // is ready in stream order.
-    return radix_sort_pairs(deg, ids, deg_sorted, plan, n, (uint32_t)std::max(0, c[2]), true, w,
-                            (int64_t)temp, stream);
+    // back above) sets the passes.  Waited for, so the plan (and the
+    // workspace) may be used from any stream once this returns.
+    const int rc = radix_sort_pairs(deg, ids, deg_sorted, plan, n, (uint32_t)std::max(0, c[2]),
+                                    true, w, (int64_t)temp, stream);
+    if (rc != SGC_OK) return rc;
+    SGC_HIP_CHECK(hipStreamSynchronize(stream));
+    return SGC_OK;
 }
 
 SGC_WARM_UNIT(warm_plan)

@@ -119,11 +119,16 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(
 // owns the K column groups {w, w+4, ...} of 16*V columns each.  MFMA k-step =
 // 4 rows: A[i=class][k=row] = G[row][class] (lane l: G[r0+(l>>4)][n*16+(l&15)]),
 // B[k=row][j] = X[r0+(l>>4)][c0 + (l&15)*V + v] for MFMA v.
+// Classes >= C read as 0 (G may be a caller's [M][C] gradient, ldg = C).
+// db_slab (nullable): wave 0's first column group also sums its block's G
+// rows per class (lane groups in row order, then across them) into
+// db_slab[blk][C16] -- db = sum_m G_m from the same loads, in a fixed order.
 template <int V, int NT, int CT>
 __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ X, int64_t ldx,
                                                      const float *__restrict__ G, int ldg, int M,
-                                                     int K, int rows_per,
-                                                     float *__restrict__ slab) {
+                                                     int K, int C, int rows_per,
+                                                     float *__restrict__ slab,
+                                                     float *__restrict__ db_slab) {
     using VT = typename Vec<V>::T;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -153,15 +158,23 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
         // r_end only occur in the ragged last step, which zeroes their G.
         float ga[NT], gn[NT];
         VT xb[CT], xn[CT];
+        const bool sum_db = db_slab && gb == 0;  // wave 0, first column group: every row once
+        float dba[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) dba[n] = 0.f;
         auto load = [&](int r0, float (&gd)[NT], VT (&xd)[CT]) {
             const int64_t r = r0 + g;
 #pragma unroll
-            for (int n = 0; n < NT; ++n) gd[n] = G[r * ldg + n * 16 + i];
+            for (int n = 0; n < NT; ++n) gd[n] = (n * 16 + i < C) ? G[r * ldg + n * 16 + i] : 0.f;
             const float *xr = X + r * ldx;
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) xd[ct] = *reinterpret_cast<const VT *>(xr + coff[ct]);
         };
         auto mma = [&](const float (&gd)[NT], const VT (&xd)[CT]) {
+            if (sum_db) {
+#pragma unroll
+                for (int n = 0; n < NT; ++n) dba[n] += gd[n];
+            }
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
@@ -190,11 +203,20 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
             const bool rok = r < r_end;
             const int64_t rr = rok ? r : r_begin;
 #pragma unroll
-            for (int n = 0; n < NT; ++n) ga[n] = rok ? G[rr * ldg + n * 16 + i] : 0.f;
+            for (int n = 0; n < NT; ++n) ga[n] = (rok && n * 16 + i < C) ? G[rr * ldg + n * 16 + i] : 0.f;
             const float *xr = X + rr * ldx;
 #pragma unroll
             for (int ct = 0; ct < CT; ++ct) xb[ct] = *reinterpret_cast<const VT *>(xr + coff[ct]);
             mma(ga, xb);
+        }
+        if (sum_db) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                float v = dba[n];
+                v += __shfl_xor(v, 16, 64);
+                v += __shfl_xor(v, 32, 64);
+                if (g == 0) db_slab[(int64_t)blockIdx.x * (NT * 16) + n * 16 + i] = v;
+            }
         }
         // D[class = 4*(l>>4)+q][j = l&15] of MFMA (n, ct, v) -> column c(j) + v
 #pragma unroll
@@ -287,11 +309,11 @@ hipError_t launch_fwd(const float *X, int64_t ldx, const float *W, const float *
 }
 
 template <int V, int NT>
-hipError_t launch_dw(const float *X, int64_t ldx, const float *G, int ldg, int M, int K,
-                     int n_slabs, int rows_per, float *slab, hipStream_t s) {
+hipError_t launch_dw(const float *X, int64_t ldx, const float *G, int ldg, int M, int K, int C,
+                     int n_slabs, int rows_per, float *slab, float *db_slab, hipStream_t s) {
     constexpr int CT = (NT >= 3) ? 2 : 4;
     hipLaunchKernelGGL((xent_dw_kernel<V, NT, CT>), dim3(n_slabs), dim3(256), 0, s, X, ldx, G,
-                       ldg, M, K, rows_per, slab);
+                       ldg, M, K, C, rows_per, slab, db_slab);
     return hipGetLastError();
 }
 
@@ -345,23 +367,23 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
     switch (NT) {                                                                                \
         case 1: e = launch_fwd<VV, 1>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,      \
                                       loss_part, db_part, logits, ldl, s);                       \
-            if (e == hipSuccess) e = launch_dw<VV, 1>(X, ldx, G, C16, (int)M, (int)K, n_slabs,   \
-                                                      rows_per, slab, s);                        \
+            if (e == hipSuccess) e = launch_dw<VV, 1>(X, ldx, G, C16, (int)M, (int)K, C16,    \
+                                                      n_slabs, rows_per, slab, nullptr, s);                        \
             break;                                                                               \
         case 2: e = launch_fwd<VV, 2>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,      \
                                       loss_part, db_part, logits, ldl, s);                       \
-            if (e == hipSuccess) e = launch_dw<VV, 2>(X, ldx, G, C16, (int)M, (int)K, n_slabs,   \
-                                                      rows_per, slab, s);                        \
+            if (e == hipSuccess) e = launch_dw<VV, 2>(X, ldx, G, C16, (int)M, (int)K, C16,    \
+                                                      n_slabs, rows_per, slab, nullptr, s);                        \
             break;                                                                               \
         case 3: e = launch_fwd<VV, 3>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,      \
                                       loss_part, db_part, logits, ldl, s);                       \
-            if (e == hipSuccess) e = launch_dw<VV, 3>(X, ldx, G, C16, (int)M, (int)K, n_slabs,   \
-                                                      rows_per, slab, s);                        \
+            if (e == hipSuccess) e = launch_dw<VV, 3>(X, ldx, G, C16, (int)M, (int)K, C16,    \
+                                                      n_slabs, rows_per, slab, nullptr, s);                        \
             break;                                                                               \
         default: e = launch_fwd<VV, 4>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,     \
                                        loss_part, db_part, logits, ldl, s);                      \
-            if (e == hipSuccess) e = launch_dw<VV, 4>(X, ldx, G, C16, (int)M, (int)K, n_slabs,   \
-                                                      rows_per, slab, s);                        \
+            if (e == hipSuccess) e = launch_dw<VV, 4>(X, ldx, G, C16, (int)M, (int)K, C16,    \
+                                                      n_slabs, rows_per, slab, nullptr, s);                        \
             break;                                                                               \
     }
     if (V == 4) {
@@ -380,6 +402,82 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
     hipLaunchKernelGGL(xent_reduce_small_kernel, dim3((unsigned)C + 1), dim3(256), 0, s, loss_part, db_part,
                        waves, (int)C, C16, 1.0 / (double)M, loss, db);
     SGC_HIP_CHECK(hipGetLastError());
+    return SGC_OK;
+}
+
+// Backward of the classifier forward Y = X W^T + b (reference models.py:18,
+// what autograd runs after F.cross_entropy(model(x), y).backward() in the
+// closures of citation.py:47-49 / reddit.py:55-58): dW = dY^T X and
+// db = sum_m dY_m from ONE read of X -- the dW slab kernel of the fused step
+// with the caller's dY as G (classes past C masked) and the db column sums
+// taken from the same G loads, then the two fixed-order reductions.
+int64_t linear_backward_workspace_bytes(int64_t M, int64_t K, int64_t C) {
+    if (M <= 0 || K <= 0 || C <= 0) return 0;
+    const int64_t C16 = (C + 15) / 16 * 16;
+    const int64_t n_slabs = std::min<int64_t>(512, (M + 255) / 256);
+    auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+    return al(n_slabs * C16 * K * 4) + al(n_slabs * C16 * 4) + 512;
+}
+
+int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ldd, int64_t M,
+                        int64_t K, int64_t C, float *dW, float *db, void *ws, int64_t ws_bytes,
+                        hipStream_t s) {
+    SGC_REQUIRE(X && dY && dW && ws, SGC_EINVAL, "linear_backward: null pointer");
+    SGC_REQUIRE(M > 0 && K > 0 && C > 0 && C <= 64 && ldx >= K && ldd >= C, SGC_EINVAL,
+                "linear_backward: bad shape M=%lld K=%lld C=%lld (C <= 64)", (long long)M,
+                (long long)K, (long long)C);
+    SGC_REQUIRE(M < INT32_MAX && K < INT32_MAX && ldd < INT32_MAX, SGC_ERANGE,
+                "linear_backward: too large");
+    const int64_t need = linear_backward_workspace_bytes(M, K, C);
+    SGC_REQUIRE(ws_bytes >= need, SGC_ENOMEM, "linear_backward: workspace %lld < %lld",
+                (long long)ws_bytes, (long long)need);
+    const int NT = (int)((C + 15) / 16);
+    const int C16 = NT * 16;
+    const int n_slabs = (int)std::min<int64_t>(512, (M + 255) / 256);
+    const int rows_per = (int)(((M + n_slabs - 1) / n_slabs + 3) / 4 * 4);
+    auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
+    char *p = (char *)(((uintptr_t)ws + 255) & ~uintptr_t(255));
+    float *slab = (float *)p;
+    p += al((int64_t)n_slabs * C16 * K * 4);
+    float *db_slab = db ? (float *)p : nullptr;
+    int V = 1;
+    for (int v : {4, 2})
+        if (K % v == 0 && ldx % v == 0 && (uintptr_t)X % (4 * v) == 0) {
+            V = v;
+            break;
+        }
+    hipError_t e = hipSuccess;
+#define SGC_BWD_DISPATCH(VV)                                                                     \
+    switch (NT) {                                                                                \
+        case 1: e = launch_dw<VV, 1>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,      \
+                                     rows_per, slab, db_slab, s); break;                         \
+        case 2: e = launch_dw<VV, 2>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,      \
+                                     rows_per, slab, db_slab, s); break;                         \
+        case 3: e = launch_dw<VV, 3>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,      \
+                                     rows_per, slab, db_slab, s); break;                         \
+        default: e = launch_dw<VV, 4>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,     \
+                                      rows_per, slab, db_slab, s); break;                        \
+    }
+    if (V == 4) {
+        SGC_BWD_DISPATCH(4)
+    } else if (V == 2) {
+        SGC_BWD_DISPATCH(2)
+    } else {
+        SGC_BWD_DISPATCH(1)
+    }
+#undef SGC_BWD_DISPATCH
+    SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear_backward launch failed: %s",
+                hipGetErrorString(e));
+    const int64_t ck = C * K;
+    hipLaunchKernelGGL(xent_reduce_dw_kernel, dim3((unsigned)((ck + 63) / 64)), dim3(256), 0, s,
+                       slab, n_slabs, (int)C, (int)K, C16, dW);
+    SGC_HIP_CHECK(hipGetLastError());
+    if (db) {  // blocks c < C reduce db_slab's column c over the slabs (no loss block)
+        hipLaunchKernelGGL(xent_reduce_small_kernel, dim3((unsigned)C), dim3(256), 0, s,
+                           (const double *)nullptr, db_slab, n_slabs, (int)C, C16, 1.0, nullptr,
+                           db);
+        SGC_HIP_CHECK(hipGetLastError());
+    }
     return SGC_OK;
 }
 

@@ -4,9 +4,11 @@ SGC (reference models.py:7-18) is logistic regression over the propagated
 features: an nn.Linear(nfeat, nclass) held as attribute `.W` (callers and
 optimisers see the same parameters: .W.weight [nclass, nfeat], .W.bias).
 On ROCm tensors the forward GEMM runs on the fp32 MFMA kernel
-(sgc_linear_f32); the backward (dW = dY^T X, db = sum dY, dX = dY W) is three
-small torch ops, so Adam (citation.py:41) and LBFGS (reddit.py:52) work
-unchanged.  On CPU tensors (the reference's --no-cuda mode) the forward is the
+(sgc_linear_f32) and the weight backward (dW = dY^T X and db = sum dY, from
+one read of X: sgc_linear_backward_f32) on the same MFMA tile -- what the
+reference closures' .backward() needs (citation.py:47-49, reddit.py:55-58);
+dX = dY W (only if the features require a gradient) is a torch op.  Adam
+(citation.py:41) and LBFGS (reddit.py:52) work unchanged.  On CPU tensors (the reference's --no-cuda mode) the forward is the
 reference's own nn.Linear arithmetic, so CPU runs reproduce its results bit
 for bit.
 """
@@ -15,6 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .propagate import linear as _mfma_linear
+from .propagate import linear_backward as _mfma_linear_backward
 from .propagate import linear_xent as _fused_xent
 
 
@@ -29,8 +32,16 @@ class _LinearMFMA(torch.autograd.Function):
     def backward(ctx, grad_out):
         x, weight = ctx.saved_tensors
         gx = grad_out @ weight if ctx.needs_input_grad[0] else None
-        gw = grad_out.t() @ x if ctx.needs_input_grad[1] else None
-        gb = grad_out.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gw = gb = None
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or want_b:
+            if weight.shape[0] <= 64:
+                gw, gb = _mfma_linear_backward(x, grad_out, want_bias=want_b)
+            else:  # wider than the fused kernel's 64 classes
+                gw = grad_out.t() @ x
+                gb = grad_out.sum(0) if want_b else None
+            if not ctx.needs_input_grad[1]:
+                gw = None
         return gx, gw, gb
 
 

@@ -605,7 +605,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                                              _lib.ptr(out), out.stride(0), F, int(K), _lib.ptr(ws),
                                              ws_bytes, cpu_threads()), "propagate_f32_cpu")
         return out
-    G = column_groups_for(csr, F) if use_plan and not native_loop else 1
+    G = column_groups_for(csr, F) if use_plan else 1
     if G > 1:
         pl = None
         parts = [(c, c.plan(0, n, threshold, hub_threshold, F)) for c in csr.column_groups(G)]
@@ -618,14 +618,26 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
     stream = _lib.stream_handle(X.device)
     ldw = aligned_ld(F)
     with torch.cuda.device(X.device):
-        if native_loop:
+        if native_loop:  # the same loop inside one C ABI call (sgc_propagate_groups_f32)
+            import ctypes
+            Gn = len(parts)
             ws_bytes = lib.sgc_propagate_workspace(n, F, X.stride(0), K)
             ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8, device=X.device)
-            _lib.check(lib.sgc_propagate_f32(_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx),
-                                             _lib.ptr(csr.val), n, _lib.ptr(X), X.stride(0),
-                                             _lib.ptr(out), out.stride(0), F, int(K),
-                                             _lib.ptr(pl.rows), pl.n_heavy, pl.n_hub, pl.threshold,
-                                             _lib.ptr(ws), ws_bytes, stream), "propagate_f32")
+            planned = use_plan and all(cp.rows is not None for _, cp, _ in parts)
+            plans = (ctypes.c_void_p * Gn)(*[cp.rows.data_ptr() if planned else None
+                                             for _, cp, _ in parts])
+            n_heavy = (ctypes.c_int64 * Gn)(*[cp.n_heavy for _, cp, _ in parts])
+            n_hub = (ctypes.c_int64 * Gn)(*[cp.n_hub for _, cp, _ in parts])
+            ths = (ctypes.c_int32 * Gn)(*[cp.threshold for _, cp, _ in parts])
+            pflags = (ctypes.c_uint32 * Gn)(*[cp.hub_flags() for _, cp, _ in parts])
+            row_ptrs = parts[0][0].row_ptr  # groups: row 0 of the [G, n+1] row_ptrs tensor
+            _lib.check(lib.sgc_propagate_groups_f32(
+                Gn, _lib.ptr(row_ptrs), _lib.ptr(parts[0][0].col_idx), _lib.ptr(parts[0][0].val), n,
+                _lib.ptr(X), X.stride(0), _lib.ptr(out), out.stride(0), F, int(K),
+                ctypes.cast(plans, ctypes.c_void_p) if planned else None,
+                ctypes.cast(n_heavy, ctypes.c_void_p), ctypes.cast(n_hub, ctypes.c_void_p),
+                ctypes.cast(ths, ctypes.c_void_p), ctypes.cast(pflags, ctypes.c_void_p),
+                _lib.ptr(ws), ws_bytes, stream), "propagate_groups_f32")
             return out
         pad = _needs_pad(X) and pad_pays(csr, F)
         # buffers actually used: the re-laid X_0 (if any) + up to two
@@ -724,6 +736,18 @@ def warmup(device=None, units=WARM_PROPAGATE | WARM_CLASSIFIER):
     t = time.perf_counter()
     with torch.cuda.device(dev):
         _lib.check(lib.sgc_warmup(int(units), _lib.stream_handle(dev)), "warmup")
+        if units & WARM_PROPAGATE:
+            # one tiny propagation through the same steps as sgc_precompute's
+            # one-GPU path, so the torch kernels they use (COO accessors,
+            # indexing, allocation) load here as well; the COO is row-unsorted
+            # (the ingest's sort runs too).  No process-group step: under
+            # torchrun every rank warms on its own.
+            n = 64
+            i = torch.arange(n, device=dev)
+            idx = torch.stack([torch.cat([(i + 1) % n, i]), torch.cat([i, i])])
+            adj = torch.sparse_coo_tensor(idx, torch.full((2 * n,), 0.5, device=dev), (n, n))
+            propagate(csr_of(adj), torch.ones((n, 8), device=dev), 2)
+        torch.cuda.synchronize(dev)
     _warmed[key] = time.perf_counter() - t
     return _warmed[key]
 
@@ -796,6 +820,39 @@ def linear(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
                                       _lib.ptr(out), out.stride(0), M, K, C,
                                       _lib.stream_handle(X.device)), "linear_f32")
     return out
+
+
+def linear_backward(X: torch.Tensor, grad_out: torch.Tensor, want_bias=True):
+    """(dW, db) of Y = X W^T + b for dY = grad_out: dW = dY^T X, db = sum_m dY
+    (None unless want_bias), one read of X on fp32 MFMA
+    (sgc_linear_backward_f32).  At most 64 classes."""
+    _require_device(X, "input")
+    M, K = X.shape
+    C = grad_out.shape[1]
+    if grad_out.shape[0] != M or X.dtype != torch.float32 or grad_out.dtype != torch.float32:
+        raise RuntimeError("sgc_amd.linear_backward: shape/dtype mismatch")
+    if C > 64:
+        raise ValueError("sgc_amd.linear_backward: at most 64 classes")
+    if X.stride(1) != 1 or X.stride(0) < K:
+        X = X.contiguous()
+    if grad_out.stride(1) != 1 or grad_out.stride(0) < C:
+        grad_out = grad_out.contiguous()
+    dW = torch.empty((C, K), dtype=torch.float32, device=X.device)
+    db = torch.empty(C, dtype=torch.float32, device=X.device) if want_bias else None
+    if M == 0:
+        dW.zero_()
+        if db is not None:
+            db.zero_()
+        return dW, db
+    lib = _lib.load()
+    ws_bytes = lib.sgc_linear_backward_workspace(M, K, C)
+    ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8, device=X.device)
+    with torch.cuda.device(X.device):
+        _lib.check(lib.sgc_linear_backward_f32(_lib.ptr(X), X.stride(0), _lib.ptr(grad_out),
+                                               grad_out.stride(0), M, K, C, _lib.ptr(dW),
+                                               _lib.ptr(db), _lib.ptr(ws), ws_bytes,
+                                               _lib.stream_handle(X.device)), "linear_backward_f32")
+    return dW, db
 
 
 def linear_xent(X: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],

@@ -118,8 +118,9 @@ def test_sgc_precompute_with_device_set_env(tiny_cases, oracle, monkeypatch):
 
 @pytest.mark.slow
 def test_mgpu_engine_reddit_shape_hash(shapes_golden):
-    """Eight virtual devices at full Reddit shape (76-column blocks): the
-    reference's X_2 hash."""
+    """1, 2 and 8 virtual devices at full Reddit shape (602-, 304- and
+    76-column blocks: the first two run two column groups per hop inside the
+    engine, the last one launch): the reference's X_2 hash each time."""
     from sgc_amd import graphs
     from sgc_amd.multigpu import DeviceSet
     from sgc_amd.propagate import DeviceCSR
@@ -128,10 +129,36 @@ def test_mgpu_engine_reddit_shape_hash(shapes_golden):
     X = torch.from_numpy(graphs.synthetic_features("reddit", g["n"], g["features"],
                                                    seed=g["feature_seed"])).cuda()
     csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device="cuda")
-    out = torch.empty_like(X)
-    DeviceSet.get([0] * 8).propagate(csr, X, 2, out)
+    for ndev in (1, 2, 8):
+        out = torch.empty_like(X)
+        DeviceSet.get([0] * ndev).propagate(csr, X, 2, out)
+        torch.cuda.synchronize()
+        got = hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()
+        assert got == g["outputs"]["2"]["sha"], ndev
+
+
+def test_mgpu_handles_survive_reinit(tiny_cases, oracle):
+    """Handles are unique for the process: an adjacency attached to an
+    engine that was since re-initialised (another device list) is detached
+    by its finalizer without touching the adjacency attached to the new
+    engine under the same ordinal."""
+    import gc
+    from sgc_amd.multigpu import DeviceSet
+    a = tiny_cases["norm_n48_F130"]
+    b = tiny_cases["norm_n48_F65"]
+    csr_a = _csr(a, oracle)
+    DeviceSet.get([0, 0]).propagate(csr_a, torch.from_numpy(a["X"]).cuda(), 2,
+                                    torch.empty(a["X"].shape, device="cuda"))
+    csr_b = _csr(b, oracle)
+    ds = DeviceSet.get([0, 0, 0])  # re-init: a's handle is void now
+    Xb = torch.from_numpy(b["X"]).cuda()
+    ds.propagate(csr_b, Xb, 2, torch.empty(b["X"].shape, device="cuda"))
+    del csr_a
+    gc.collect()  # a's finalizer detaches a's (old) handle
+    out = torch.full(b["X"].shape, float("nan"), device="cuda")
+    ds.propagate(csr_b, Xb, 2, out)
     torch.cuda.synchronize()
-    assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == g["outputs"]["2"]["sha"]
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), b["Y2"].view(np.uint32))
 
 
 # ---------------------------------------------------------------------------

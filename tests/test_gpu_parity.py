@@ -526,6 +526,31 @@ def test_sgc_model_autograd_matches_torch():
 
 
 @pytest.mark.parametrize("M,K,C", [(1, 3, 2), (140, 1433, 7), (333, 602, 41), (1000, 500, 3),
+                                   (4099, 602, 41), (77, 64, 64), (600, 130, 17), (152410, 602, 41),
+                                   (5, 601, 1)])
+def test_linear_backward_matches_torch(M, K, C):
+    """sgc_linear_backward_f32 (the SGC.forward backward: dW = dY^T X, db =
+    sum dY from one read of X) vs fp64 torch, fp32 tolerance; dY a caller's
+    [M, C] tensor (classes not a multiple of 16 are masked in the kernel);
+    bitwise reproducible run to run."""
+    from sgc_amd.propagate import linear_backward
+    g = torch.Generator().manual_seed(M + 3 * K + C)
+    X = torch.randn((M, K), generator=g)
+    dY = torch.randn((M, C), generator=g) / M
+    dW, db = linear_backward(X.to(DEV), dY.to(DEV))
+    wref = dY.double().t() @ X.double()
+    bref = dY.double().sum(0)
+    torch.testing.assert_close(dW.cpu().double(), wref, rtol=1e-4,
+                               atol=1e-5 * max(1e-3, wref.abs().max().item()))
+    torch.testing.assert_close(db.cpu().double(), bref, rtol=1e-4,
+                               atol=1e-5 * max(1e-3, bref.abs().max().item()))
+    dW2, db2 = linear_backward(X.to(DEV), dY.to(DEV))
+    assert torch.equal(dW, dW2) and torch.equal(db, db2)
+    dW3, none = linear_backward(X.to(DEV), dY.to(DEV), want_bias=False)
+    assert none is None and torch.equal(dW, dW3)
+
+
+@pytest.mark.parametrize("M,K,C", [(1, 3, 2), (140, 1433, 7), (333, 602, 41), (1000, 500, 3),
                                    (4099, 602, 41), (77, 64, 64), (600, 130, 17)])
 def test_fused_xent_matches_torch(M, K, C):
     """loss, dW, db of the fused training step vs fp64 torch (fp32 tolerance)."""
@@ -769,7 +794,8 @@ def test_column_groups_tiny_cases_bit_exact(tiny_cases, G, monkeypatch):
 def test_column_groups_medium_graph_bit_exact(oracle, F):
     """The default rule on a 4.2 M-nonzero graph (two groups at 128 and
     > 256 floats, one at 129-256), forced 1, 3 and 4 groups, split hops (spmm over a row range) and
-    the one-launch schedule: the oracle's bits."""
+    the one-launch schedule, the Python hop loop and the native one
+    (sgc_propagate_groups_f32): the oracle's bits."""
     from sgc_amd import graphs
     import importlib
     prop_mod = importlib.import_module("sgc_amd.propagate")
@@ -788,9 +814,11 @@ def test_column_groups_medium_graph_bit_exact(oracle, F):
         for G in (None, 1, 3, 4):
             prop_mod.COLUMN_GROUPS = G
             out = propagate(csr, Xd, 2)
+            native = propagate(csr, Xd, 2, native_loop=True)  # sgc_propagate_groups_f32
             part = spmm(csr, Xd, 1000, 37000)
             torch.cuda.synchronize()
             assert bits_equal(out.cpu().numpy(), want2), (F, G)
+            assert bits_equal(native.cpu().numpy(), want2), (F, G, "native")
             assert bits_equal(part.cpu().numpy(), want1[1000:37000]), (F, G)
     finally:
         prop_mod.COLUMN_GROUPS = saved
