@@ -12,8 +12,12 @@ Metric (BASELINE.json): propagated edges/s = hops * nnz(S) / t, where t is
 one sgc_precompute (all K hops of S.X, reference utils.py:92-97) over the
 synthetic Reddit-shape graph (232,965 nodes, 11,606,919 undirected edges,
 nnz(S) = 23,446,803, F = 602, K = 2), inputs resident in HBM.
-A "step" = one full K-hop propagation.  N > 1 (sgc_amd.distributed), total
-work fixed, so scaling is "strong":
+A "step" = one full K-hop propagation.  N > 1: `value` times the SAME call
+as N = 1 -- sgc_precompute(features, adj, K) on every rank under the process
+group (sgc_amd.multigpu: partitioned hops, every rank gets the whole X_K, as
+the reference returns it; partition SGC_AMD_PARTITION, default features);
+total work fixed, so scaling is "strong".  Beside it (`sharded_output`) the
+partitioned propagator with sharded output (sgc_amd.distributed):
   --partition rows  S row-partitioned (nnz-balanced row blocks, SURVEY.md
                 8(e)); RCCL all-gather of X_k after each hop that feeds another,
                 optionally pipelined in feature groups, hub rows on their own streams
@@ -27,9 +31,6 @@ work fixed, so scaling is "strong":
                 output by one all-to-all of the row blocks of X_K
   --partition auto (default)  rows vs cyclic vs features (vs tiles), timed
                 on the node (max over ranks); the fastest is kept
-  --output sharded (default)  each rank ends with its row block of X_K
-  --output replicated  every rank ends with all of X_K (one more all-gather)
-The other output mode is timed too (`alt_output`, --alt-steps).
 
 Also printed (same JSON line, N = 1):
   roofline      the SpMM hop (spmm_rows_kernel / spmm_csr_kernel, joined with
@@ -563,15 +564,11 @@ def main():
     ap.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "pairwise"],
                     help="feature partition, sharded output: all-to-all after the last hop, or "
                          "pairwise P2P overlapped with it (auto: pairwise at N = 2)")
-    ap.add_argument("--output", default="sharded", choices=["sharded", "replicated"],
-                    help="N>1: each rank keeps its row block of X_K, or all ranks get all of it")
     ap.add_argument("--chunks", type=int, default=4,
                     help="N>1 features, replicated output: row chunks of the last hop")
-    ap.add_argument("--alt-steps", type=int, default=5,
-                    help="N>1: steps timed with the other output mode (0 = skip)")
-    ap.add_argument("--public-steps", type=int, default=5,
-                    help="N>1: steps timed through the public sgc_precompute under the process "
-                         "group (replicated X_K, sgc_amd.multigpu; 0 = skip)")
+    ap.add_argument("--sharded-steps", type=int, default=5,
+                    help="N>1: steps timed beside the public call with the partitioned "
+                         "propagator and sharded output (0 = skip)")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
                     help="schedule knob for sgc_set_tuning (results never depend on it)")
     args = ap.parse_args()
@@ -647,90 +644,107 @@ def main():
     X_host = graphs.synthetic_features(args.shape, S.n, spec["features"], seed=args.seed + 1)
     n, F, nnz = S.n, X_host.shape[1], S.nnz
     X0 = torch.from_numpy(X_host).to(dev)
-    tm = {"on": False, "pairs": [], "bytes": []}
-    if args.partition == "auto":
-        # row partition vs 2-D tiles: timed on this node (max over ranks), so
-        # the exchange rate the node actually has decides, not an estimate
-        import copy
-        cands = ["rows", "cyclic", "features"]
-        if world >= 4 and world % args.col_blocks == 0 and args.output == "sharded":
-            cands.append("tiles")
-        trials = {}
-        for cand in cands:
-            a = copy.copy(args)
-            a.partition = cand
-            t_c = {"on": False, "pairs": [], "bytes": []}
-            built = build_dist_step(a, S, X0, dev, rank, world, K, args.output, t_c)
-            e_c, _, _ = timed(built[0], 3, 1, True, dev)
-            trials[cand] = (e_c / 3, built, t_c)
-        best = min(trials, key=lambda c: (trials[c][0], c))
-        chosen = best
-        _, (step, parallelism, unit_desc), tm = trials[best]
-        parallelism += " [auto-selected: " + ", ".join(
-            f"{c} {trials[c][0] * 1e3:.2f} ms" for c in cands) + "]"
-    else:
-        chosen = args.partition
-        step, parallelism, unit_desc = build_dist_step(args, S, X0, dev, rank, world, K,
-                                                       args.output, tm)
-    elapsed, step_ms, _ = timed(step, args.steps, args.warmup, True, dev,
-                                on_start=lambda: tm.update(on=True),
-                                on_stop=lambda: tm.update(on=False))
-    launch_ms = [s.elapsed_time(e) for s, e in tm["pairs"]]
-    alt = None
-    if args.alt_steps > 0 and chosen != "tiles":  # tiles: sharded output only
-        import copy
-        a = copy.copy(args)
-        a.partition = chosen
-        alt_mode = "replicated" if args.output == "sharded" else "sharded"
-        alt_step, alt_par, _ = build_dist_step(a, S, X0, dev, rank, world, K, alt_mode,
-                                               {"on": False})
-        e_alt, _, _ = timed(alt_step, args.alt_steps, 1, True, dev)
-        alt = {"output": alt_mode, "parallelism": alt_par, "steps": args.alt_steps,
-               "ms_per_step": e_alt * 1e3 / args.alt_steps,
-               "value": K * nnz * args.alt_steps / e_alt}
-    public = None
-    if args.public_steps > 0:
-        # the reference's own call, unchanged, under this process group:
-        # sgc_precompute(features, adj, K) -> every rank gets all of X_K
-        from sgc_amd import multigpu
-        from sgc_amd.utils import sgc_precompute
-        rows_, cols_, vals_ = S.coo()
-        adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([rows_, cols_])),
-                                      torch.from_numpy(vals_), (n, n)).to(dev)
-        del rows_, cols_, vals_
-        torch.cuda.synchronize()
-        _, first_pub = sgc_precompute(X0, adj, K)  # ingest + partition set-up
-        e_pub, _, _ = timed(lambda: sgc_precompute(X0, adj, K)[0], args.public_steps, 1, True,
-                            dev)
-        public = {"call": "sgc_precompute(features, adj, K) on every rank (sgc_amd.utils -> "
-                          "sgc_amd.multigpu): replicated X_K", "partition": multigpu.partition_name(),
-                  "steps": args.public_steps, "ms_per_step": e_pub * 1e3 / args.public_steps,
-                  "value": K * nnz * args.public_steps / e_pub,
-                  "first_call_seconds": round(first_pub, 4)}
-        del adj
+    # value: the SAME call as N = 1 -- the reference's sgc_precompute(features,
+    # adj, K), unchanged, on every rank under this process group
+    # (sgc_amd.utils -> sgc_amd.multigpu: partitioned hops, every rank gets
+    # the whole X_K as the reference returns it)
+    from sgc_amd import multigpu
+    from sgc_amd.distributed import feature_bounds
+    from sgc_amd.propagate import warmup
+    from sgc_amd.utils import sgc_precompute
+    rows_, cols_, vals_ = S.coo()
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([rows_, cols_])),
+                                  torch.from_numpy(vals_), (n, n)).to(dev)
+    del rows_, cols_, vals_
+    torch.cuda.synchronize()
+    warm_s = warmup(dev)  # what the drop-in loaders do on every rank
+    _, first_pub = sgc_precompute(X0, adj, K)  # ingest + partition set-up + K hops
+    partition = multigpu.partition_name()
+    launches = LaunchTimer(1)
+
+    def public_step():
+        return sgc_precompute(X0, adj, K)[0]
+    elapsed, step_ms, _ = timed(public_step, args.steps, args.warmup, True, dev)
+    # the same steps again with the library's per-launch events (rank 0's
+    # launches: the roofline's kernel and times; label from the library)
+    elapsed_i, _, extra = timed(public_step, args.steps, 1, True, dev,
+                                on_start=launches.start if rank == 0 else None,
+                                on_stop=launches.stop if rank == 0 else None)
+    span, light, hub, kernel = extra if extra else (None, None, None, None)
+    sharded = None
+    if args.sharded_steps > 0:
+        # beside it: the partitioned propagator with SHARDED output (each rank
+        # keeps its row block of X_K, as a data-parallel classifier would
+        # consume it), partition timed on the node (--partition auto)
+        tm = {"on": False, "pairs": [], "bytes": []}
+        if args.partition == "auto":
+            import copy
+            cands = ["rows", "cyclic", "features"]
+            if world >= 4 and world % args.col_blocks == 0:
+                cands.append("tiles")
+            trials = {}
+            for cand in cands:
+                a = copy.copy(args)
+                a.partition = cand
+                built = build_dist_step(a, S, X0, dev, rank, world, K, "sharded",
+                                        {"on": False, "pairs": [], "bytes": []})
+                e_c, _, _ = timed(built[0], 2, 1, True, dev)
+                trials[cand] = (e_c / 2, built)
+            chosen = min(trials, key=lambda c: (trials[c][0], c))
+            step, par, _ = trials[chosen][1]
+            par += " [auto-selected: " + ", ".join(f"{c} {trials[c][0] * 1e3:.2f} ms"
+                                                   for c in cands) + "]"
+        else:
+            step, par, _ = build_dist_step(args, S, X0, dev, rank, world, K, "sharded", tm)
+        e_sh, _, _ = timed(step, args.sharded_steps, 1, True, dev)
+        sharded = {"output": "sharded (each rank: its row block of X_K)", "parallelism": par,
+                   "steps": args.sharded_steps, "ms_per_step": e_sh * 1e3 / args.sharded_steps,
+                   "value": K * nnz * args.sharded_steps / e_sh,
+                   "what": "the partitioned propagator without the final replication; not the "
+                           "reference's call"}
     if rank == 0:
+        fb, B = feature_bounds(F, world)
+        par = (f"{partition}-partition x{world} via sgc_precompute under the process group "
+               f"({'RCCL over xGMI' if args.dist_backend == 'nccl' else 'gloo rehearsal'}); "
+               f"output replicated (every rank gets all of X_K, as the reference returns it)")
         rec.update({"value": K * nnz * args.steps / elapsed,
                     "ms_per_step": elapsed * 1e3 / args.steps,
                     "ms_per_step_median_rank0": float(np.median(step_ms)),
+                    "ms_per_step_instrumented": elapsed_i * 1e3 / args.steps,
                     "config": {"workload": f"{args.shape}-shape sgc_precompute K={K}", "nodes": n,
                                "undirected_edges": spec["edges"], "nnz": nnz, "features": F,
-                               "hops": K, "parallelism": parallelism, "launch_unit": unit_desc},
+                               "hops": K, "parallelism": par, "output": "replicated",
+                               "partition": partition},
+                    "timed_call": "sgc_precompute(features, adj, K) (sgc_amd.utils, the drop-in), "
+                                  "every rank, the same call as N = 1",
+                    "first_call_seconds": round(first_pub, 4),
+                    "loader_warmup_seconds": round(warm_s, 4),
                     "lib_sha256": lib_sha})
-        if launch_ms:
-            t_l = float(np.mean(launch_ms)) * 1e-3
-            b_l = float(np.mean(tm["bytes"]))
+        if span:
+            # rank 0's SpMM launches; at the feature partition a launch is one
+            # hop over all rows at the rank's block width -- the compulsory
+            # bytes (S once, the block of X once, its Y once) are the basis,
+            # the same model as N = 1's `compulsory_frac`
+            w = int(fb[1] - fb[0]) if partition == "features" else None
+            t_l = float(np.mean(span)) * 1e-3
+            cb = (4 * (n + 1) + 8 * nnz + 8 * w * n) if w else None
             rec["roofline"] = {
                 "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "achieved": b_l / t_l / 1e9, "frac": b_l / t_l / 1e9 / HBM_PEAK_GBS,
-                "traffic": None, "achieved_basis": "compulsory bytes per launch (rank 0)",
-                "kernel": "spmm_csr_kernel (+ spmm_hub_kernel, joined), rank 0's launches",
-                "kernel_mean_ms": t_l * 1e3, "launches": len(launch_ms),
-                "compulsory_bytes_per_launch": b_l}
+                "kernel": (f"{kernel} (+ spmm_hub_kernel beside it, joined)" if hub else
+                           str(kernel)),
+                "kernel_mean_ms": t_l * 1e3, "launches": len(span),
+                "launch_unit": (f"rank 0's hop over all {n} rows at its {w}-column block"
+                                if w else "rank 0's SpMM launches"),
+                "achieved": cb / t_l / 1e9 if cb else None,
+                "frac": cb / t_l / 1e9 / HBM_PEAK_GBS if cb else None,
+                "compulsory_bytes_per_launch": cb,
+                "compulsory_frac": cb / t_l / 1e9 / HBM_PEAK_GBS if cb else None,
+                "traffic": None,
+                "achieved_basis": "compulsory bytes (S, the block of X and its Y once) per launch; "
+                                  "N = 1's roofline carries the same basis as compulsory_frac"}
         rec["precompute_seconds"] = rec["ms_per_step"] / 1e3
-        if alt is not None:
-            rec["alt_output"] = alt
-        if public is not None:
-            rec["public_call"] = public
+        if sharded is not None:
+            rec["sharded_output"] = sharded
         print(json.dumps(rec), flush=True)
     dist.barrier()
     dist.destroy_process_group()

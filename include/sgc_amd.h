@@ -245,7 +245,11 @@ int sgc_timing_collect_ex(float *light_ms_host, float *hub_ms_host, float *span_
  * SGC_SPMM_X_UNDER_4G: the caller vouches that X has fewer than 2^24 rows
  * and that every X row a column id can name lies within 4 GiB of X
  * (n_cols * ldx * 4 < 2^32), so the gathers may use 32-bit row offsets from
- * one 24-bit multiply (fewer address instructions per nonzero).  */
+ * one 24-bit multiply (fewer address instructions per nonzero).  The library
+ * cannot check it (it never sees n_cols here): a caller that sets the flag
+ * for a larger X gets wrapped addresses -- wrong rows gathered -- not an
+ * error.  sgc_propagate_f32 / sgc_propagate_groups_f32 and the Python layer
+ * derive it themselves from n_rows and the row stride.  */
 enum { SGC_SPMM_X_PADDED = 1, SGC_SPMM_Y_PADDED = 2, SGC_SPMM_NO_HUB = 4,
        SGC_SPMM_HUB_ONLY = 8, SGC_SPMM_ACCUMULATE = 16, SGC_SPMM_HUB_SERIAL = 32,
        SGC_SPMM_LIGHT_ORDER = 64, SGC_SPMM_X_UNDER_4G = 128 };

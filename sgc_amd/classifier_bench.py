@@ -125,14 +125,32 @@ def classifier_record(dev, M=152410, K=602, C=41, reps=20, epochs=2, seed=0):
     return rec
 
 
+def workload(dev, M=152410, K=602, C=41, loops=20):
+    """Only the two classifier kernels, `loops` times each (rocprofv3 passes)."""
+    from .propagate import linear, linear_backward
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn(M, K, generator=g).to(dev)
+    W = (torch.randn(C, K, generator=g) * 0.05).to(dev)
+    b = torch.randn(C, generator=g).to(dev)
+    dY = torch.randn(M, C, generator=g).to(dev)
+    for _ in range(loops):
+        linear(x, W, b)
+        linear_backward(x, dY)
+    torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=152410)
     ap.add_argument("--features", type=int, default=602)
     ap.add_argument("--classes", type=int, default=41)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--workload", action="store_true", help="kernels only (profiling)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if a.workload:
+        workload(dev, a.rows, a.features, a.classes)
+        return
     print(json.dumps(classifier_record(dev, a.rows, a.features, a.classes, a.reps)), flush=True)
 
 

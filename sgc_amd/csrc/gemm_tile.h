@@ -80,25 +80,29 @@ namespace sgc {
 
 // LDS-staged block tile for the classifier GEMMs: a 256-thread block owns
 // kLdsBM = 128 rows of X and every class (NT x 16); wave w computes rows
-// [32w, 32w + 32) (MT = 2) from LDS.  Per K-chunk of 32 the block stages X
-// [128 x 32] (16 consecutive threads read one row's 128 B: coalesced) and W
-// [16NT x 32] through registers into LDS; the next chunk's global loads are in
-// flight while the current chunk's MFMAs run.  Compared with every wave
-// streaming its own W rows (xwt_tile), W leaves L2 once per block, not once
-// per wave, and X arrives in whole 128-B lines.
+// [32w, 32w + 32) (MT = 2).  Per K-chunk of 32 the block stages X [128 x 32]
+// (16 consecutive threads read one row's 128 B: coalesced) and W [16NT x 32]
+// through registers into LDS; W leaves L2 once per block, X arrives in whole
+// 128-B lines.
+//
+// Schedule (round 4; the round-1 tile measured 158 us at Reddit-train shape,
+// 31 % of the HBM roofline, with its waves 53 % issue-stalled and 36 %
+// parked on waits: profiles/r04/pmc_cls/): the LDS image is double buffered,
+// so a chunk costs ONE barrier -- chunk c+1's global loads are in flight and
+// its LDS store follows chunk c's MFMAs into the other buffer -- and a lane
+// reads its operands of the whole chunk with ds_read_b128 (k permuted: MFMA
+// step kk sums k = 8g + kk over the lane groups g, so lane l's eight k of a
+// chunk are contiguous), 10 LDS reads per 48 MFMAs instead of 40.  fp32 MFMA
+// sums exactly; the k order differs from torch's (tolerance parity).
 constexpr int kLdsBM = 128;
-#ifndef SGC_LDS_BK
-#define SGC_LDS_BK 32
-#endif
-constexpr int kLdsBK = SGC_LDS_BK;
-// LDS row stride == 2 (mod 32): the 32 lanes of a ds_read_b32 half-wave (16
-// rows x 2 adjacent k) then hit 32 distinct banks.
-constexpr int kLdsPad = kLdsBK + 2;
+constexpr int kLdsBK = 32;
+// row stride 36 floats: 16-B aligned rows for ds_read_b128 / ds_write_b64
+constexpr int kLdsPad = kLdsBK + 4;
 
 template <int V, int NT>
 struct LdsTile {
-    float xs[kLdsBM][kLdsPad];
-    float ws[NT * 16][kLdsPad];
+    float xs[2][kLdsBM][kLdsPad];
+    float ws[2][NT * 16][kLdsPad];
 };
 
 template <int V, int NT>
@@ -107,6 +111,7 @@ __device__ __forceinline__ void xwt_block_tile(const float *__restrict__ X, int6
                                                int m_blk, LdsTile<V, NT> &sm,
                                                f32x4 (&acc)[2][NT]) {
     using VT = typename Vec<V>::T;
+    typedef float f4 __attribute__((ext_vector_type(4)));
     constexpr int PER_ROW = kLdsBK / V;                      // vectors per row per chunk
     constexpr int XV = kLdsBM * PER_ROW / 256;               // X vectors per thread
     constexpr int WV = (NT * 16 * PER_ROW + 255) / 256;      // W vectors per thread
@@ -136,43 +141,51 @@ __device__ __forceinline__ void xwt_block_tile(const float *__restrict__ X, int6
             if (!ok) wr[j] = VT{};
         }
     };
-    auto store = [&]() {
+    auto store = [&](int buf) {
 #pragma unroll
         for (int j = 0; j < XV; ++j) {
             const int q = tid + 256 * j;
             const int row = q / PER_ROW, kc = (q % PER_ROW) * V;
-#pragma unroll
-            for (int v = 0; v < V; ++v) sm.xs[row][kc + v] = lane_elem<V>(xr[j], v);
+            *reinterpret_cast<VT *>(&sm.xs[buf][row][kc]) = xr[j];
         }
 #pragma unroll
         for (int j = 0; j < WV; ++j) {
             const int q = tid + 256 * j;
             if (q < NT * 16 * PER_ROW) {
                 const int c = q / PER_ROW, kc = (q % PER_ROW) * V;
-#pragma unroll
-                for (int v = 0; v < V; ++v) sm.ws[c][kc + v] = lane_elem<V>(wr[j], v);
+                *reinterpret_cast<VT *>(&sm.ws[buf][c][kc]) = wr[j];
             }
         }
     };
+    const int n_chunks = (K + kLdsBK - 1) / kLdsBK;
     load(0);
-    for (int k0 = 0; k0 < K; k0 += kLdsBK) {
-        __syncthreads();  // the previous chunk's reads of LDS are done
-        store();
-        __syncthreads();
-        if (k0 + kLdsBK < K) load(k0 + kLdsBK);  // in flight during this chunk's MFMAs
+    store(0);
+    __syncthreads();
+    for (int c = 0; c < n_chunks; ++c) {
+        const int buf = c & 1;
+        if (c + 1 < n_chunks) load((c + 1) * kLdsBK);  // in flight during this chunk
+        // this lane's 8 k of the chunk (k = 8g .. 8g+7) for its rows / classes
+        f4 a[2][2], b[NT][2];
 #pragma unroll
-        for (int kk = 0; kk < kLdsBK; kk += 4) {
-            float a[2], b[NT];
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int t = 0; t < 2; ++t) a[t] = sm.xs[w * 32 + t * 16 + i][kk + g];
+            for (int h = 0; h < 2; ++h)
+                a[t][h] = *reinterpret_cast<const f4 *>(&sm.xs[buf][w * 32 + t * 16 + i][8 * g + 4 * h]);
 #pragma unroll
-            for (int n = 0; n < NT; ++n) b[n] = sm.ws[n * 16 + i][kk + g];
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                b[n][h] = *reinterpret_cast<const f4 *>(&sm.ws[buf][n * 16 + i][8 * g + 4 * h]);
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int n = 0; n < NT; ++n)
-                    acc[t][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[n], acc[t][n], 0, 0, 0);
-        }
+                    acc[t][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        a[t][kk >> 2][kk & 3], b[n][kk >> 2][kk & 3], acc[t][n], 0, 0, 0);
+        if (c + 1 < n_chunks) store(buf ^ 1);  // the other buffer: read last chunk, barrier since
+        __syncthreads();
     }
 }
 

@@ -378,6 +378,140 @@ __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
     }
 }
 
+// Heavy row of a NARROW launch (at most 64 floats), four nonzeros per load
+// instruction: lane group g = lane / 16 gathers nonzero k+g's X segment,
+// 16 lanes x V floats (V = 4 / 2 / 1: segments of up to 64 / 32 / 16 floats),
+// so one load moves four row segments where pairs move two (at 64 floats
+// pairs leave half of each 32-lane half idle, at 32 or 12 floats three
+// quarters or more).  What bounds a narrow pass is the load instructions (a
+// wave instruction costs the texture unit about the same whether it carries
+// two or four segments: scripts/micro/gather_rate.hip, 64 floats 0.42 ms at two
+// segments per instruction vs 0.37 at four) and a long row's loads in flight
+// (4 x U x 2 here: twice the pairs').  Every lane then needs the four
+// nonzeros' values of its features, in order:
+//   v_permlane32_swap(x, x) -> t0 = x of lane L mod 32 (group 0 or 1, same
+//     16-lane position), t1 = x of lane 32 + L mod 32 (group 2 or 3);
+//   v_permlane16_swap(t, t) -> t of lane L & ~16 and of lane L | 16:
+//     groups 0, 1 from t0 and 2, 3 from t1 -- in every lane, the same order;
+// and the chain takes them in nonzero order: acc = fma(v_k, x_k, acc), ...,
+// fma(v_k+3, x_k+3, acc), the same sequential FMA chain per element (all four
+// groups compute it; group 0 stores).  The S values and column ids come from
+// the 64-nonzero (col, val) block by v_readlane (wave-uniform), the column of
+// the lane's own group by two selects.
+constexpr int kQuadsU = 4;  // quads per step (16 nonzeros; two steps = 32 in flight)
+
+template <int V, int U, bool O32>
+__device__ __forceinline__ void row_quads_pipe(const int *__restrict__ col,
+                                               const float *__restrict__ val, int k0, int k1,
+                                               const float *__restrict__ X, int64_t ldx,
+                                               float *__restrict__ yrow, int F, int f_lane,
+                                               bool lane_ok, bool vec_store, int lane,
+                                               bool accum) {
+    using VT = typename Vec<V>::T;
+    constexpr int kSteps = kWave / (4 * U);  // steps per 64-nonzero block
+    static_assert(kWave % (4 * U) == 0 && kSteps % 2 == 0, "4U must divide 64 into an even count");
+    if (accum && k1 == k0) return;
+    const int g = lane >> 4;
+    const uint32_t boff = lane_ok ? uint32_t(f_lane) * 4u : 0u;
+    VT acc;
+#pragma unroll
+    for (int v = 0; v < V; ++v) set_elem<V>(acc, v, 0.0f);
+    if (accum && lane_ok) {
+        if (vec_store) {
+            acc = *reinterpret_cast<const VT *>(yrow + f_lane);
+        } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if (f_lane + v < F) set_elem<V>(acc, v, yrow[f_lane + v]);
+        }
+    }
+    if (k1 > k0) {
+        const char *Xb = reinterpret_cast<const char *>(X);
+        const int64_t row_bytes = ldx * 4;
+        const int last = k1 - 1;
+        int colA = ld_meta(col + min(k0 + lane, last));
+        float valA = ld_meta(val + min(k0 + lane, last));
+        int colB = ld_meta(col + min(k0 + kWave + lane, last));
+        float valB = ld_meta(val + min(k0 + kWave + lane, last));
+        VT xv[2][U];
+        float vq[2][U][4];
+        auto issue = [&](int base, int i, int colr, float valr, int buf) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int kq = base + i * 4 * U + 4 * u;
+                int c[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int l = (min(kq + j, last) - base) & (kWave - 1);
+                    c[j] = __builtin_amdgcn_readlane(colr, l);
+                    vq[buf][u][j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(valr), l));
+                }
+                const int c01 = (g & 1) ? c[1] : c[0];
+                const int c23 = (g & 1) ? c[3] : c[2];
+                const int cj = (g & 2) ? c23 : c01;
+                if constexpr (O32)
+                    xv[buf][u] = *reinterpret_cast<const VT *>(
+                        Xb + (__umul24((uint32_t)cj, (uint32_t)row_bytes) + boff));
+                else
+                    xv[buf][u] = *reinterpret_cast<const VT *>(Xb + (int64_t)cj * row_bytes + boff);
+            }
+        };
+        auto step = [&](int base, int i, bool last_block) {
+            const int cur = base + i * 4 * U;
+            if (i + 1 < kSteps) {
+                issue(base, i + 1, colA, valA, (i + 1) & 1);
+            } else if (!last_block) {
+                const int nb2 = base + 2 * kWave;  // the block after next
+                const int cN = ld_meta(col + min(nb2 + lane, last));
+                const float vN = ld_meta(val + min(nb2 + lane, last));
+                issue(base + kWave, 0, colB, valB, 0);
+                colA = colB;
+                valA = valB;
+                colB = cN;
+                valB = vN;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int kq = cur + 4 * u;
+                if (kq > last) break;  // uniform
+                const int n_here = min(4, last - kq + 1);  // uniform
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    const uint32_t x = __float_as_uint(lane_elem<V>(xv[i & 1][u], v));
+                    const auto t = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+                    const auto p = __builtin_amdgcn_permlane16_swap(t[0], t[0], false, false);
+                    const auto q = __builtin_amdgcn_permlane16_swap(t[1], t[1], false, false);
+                    float a = lane_elem<V>(acc, v);
+                    a = __builtin_fmaf(vq[i & 1][u][0], __uint_as_float(p[0]), a);
+                    if (n_here > 1) a = __builtin_fmaf(vq[i & 1][u][1], __uint_as_float(p[1]), a);
+                    if (n_here > 2) a = __builtin_fmaf(vq[i & 1][u][2], __uint_as_float(q[0]), a);
+                    if (n_here > 3) a = __builtin_fmaf(vq[i & 1][u][3], __uint_as_float(q[1]), a);
+                    set_elem<V>(acc, v, a);
+                }
+            }
+        };
+        issue(k0, 0, colA, valA, 0);
+        const int nblk = (k1 - k0 + kWave - 1) / kWave;
+        int base = k0;
+        for (int b = 0; b + 1 < nblk; ++b, base += kWave) {
+#pragma unroll
+            for (int i = 0; i < kSteps; ++i) step(base, i, false);
+        }
+#pragma unroll
+        for (int i = 0; i < kSteps; ++i)  // no exit: skipped steps fall through
+            if (base + i * 4 * U <= last) step(base, i, true);
+    }
+    if (g == 0 && lane_ok) {
+        if (vec_store) {
+            *reinterpret_cast<VT *>(yrow + f_lane) = acc;
+        } else {
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+                if (f_lane + v < F) yrow[f_lane + v] = lane_elem<V>(acc, v);
+        }
+    }
+}
+
 // Grid: x = work items of one feature slice, y = slice.  Workgroups are
 // dispatched x-fastest, so the chip sweeps the slices one after another and
 // only X[:, slice] (N x 64CV floats -- 119 MB at Reddit shape for 128
@@ -468,7 +602,7 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 // slower on a 76-float slice, profiles/r02/packed_sweep.log).
 constexpr int kRowsU = 4;  // nonzeros per row per step (one b128 (col, val) read each)
 
-template <int LB, int VH, int UH, bool O32>
+template <int LB, int VH, int UH, bool O32, int QV>
 __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
@@ -492,6 +626,13 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
         const int h = wave / n_sub;
         const int row = heavy_rows[h];
         const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
+        if constexpr (QV > 0) {  // 16 lanes per row: four nonzeros per load
+            const int f = slice * (LR * V) + (lane & 15) * QV;
+            row_quads_pipe<QV, kQuadsU, O32>(col, val, k0, k1, X, ldx,
+                                             Y + (int64_t)(row - row_begin) * ldy, F, f,
+                                             f < F_load, vec_store != 0, lane, accum != 0);
+            return;
+        }
         if (heavy_pairs & 1) {  // n_sub == 1: one item per (row, slice), two nonzeros per load
             const int j = lane & 31;
             const int f = slice * (LR * V) + j * V;
@@ -1122,8 +1263,11 @@ constexpr int kHeavyU = 16;
 // Heavy rows, two nonzeros per load instruction (row_pairs_pipe, 16-B lanes)
 // instead of one wave per 64*VH-float sub-chunk (row_chunks_pipe): bit 0 = in
 // the multi-row kernel (Reddit shape K=2: 9.29 -> 9.12 ms, profiles/r03/s1/ab.log),
-// bit 1 = in the one-row kernel.  Set through sgc_set_tuning("heavy_pairs").
-static int g_heavy_pairs = 1;
+// bit 1 = in the one-row kernel; bit 2 = four nonzeros per load instead of two
+// in the multi-row kernel when a row has at most 16 lanes (launches of <= 64
+// floats, or 64-float slices: row_quads_pipe).
+// Set through sgc_set_tuning("heavy_pairs").
+static int g_heavy_pairs = 5;
 // One-row kernel: row_chunks_pipe2 (whole-block schedule) on launches of at
 // least this many rows, row_chunks_pipe below.  Measured bit-identical,
 // interleaved (profiles/r03/s5/chunks_*.log): RMAT shape K=3 (4.2 M rows)
@@ -1178,13 +1322,13 @@ static int g_rows_per_wave = 0;
 // launches (Pubmed shape, F = 500) stay latency-bound on the one-row kernel.
 constexpr int64_t kWideRowsMin = 65536;
 
-template <int LB, int VH, bool O32>
+template <int LB, int VH, bool O32, int QV>
 hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int R = kWave / LR, SW = LR * 4;
     const int slices = (F_load + SW - 1) / SW;
     // heavy sub-chunks per slice (unpacked heavy rows): whole 64*VH-float
     // chunks of a slice, or of the launch's width when it is a single slice
-    const int n_sub = (g_heavy_pairs & 1) ? 1
+    const int n_sub = (QV > 0 || (g_heavy_pairs & 1)) ? 1
                       : slices > 1 ? SW / (kWave * VH) : (F_load + kWave * VH - 1) / (kWave * VH);
     const int64_t heavy_waves = (int64_t)a.n_heavy * n_sub;
     // light items: every row (non-light rows skip themselves), or with a
@@ -1193,7 +1337,7 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int64_t waves = heavy_waves + (n_light_items + R - 1) / R;
     const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     dim3 grid((unsigned)blocks, (unsigned)slices);
-    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU, O32>), grid, dim3(kBlock), 0, a.stream,
+    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU, O32, QV>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
                        n_light_items, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
                        a.heavy_threshold, a.accum, a.light_rows, g_heavy_pairs & 1);
@@ -1274,7 +1418,7 @@ int set_tuning(const char *key, int64_t value) {
         return SGC_OK;
     }
     if (std::string(key) == "heavy_pairs") {
-        SGC_REQUIRE(value >= 0 && value <= 3, SGC_EINVAL, "heavy_pairs must be 0..3 (a bit mask)");
+        SGC_REQUIRE(value >= 0 && value <= 7, SGC_EINVAL, "heavy_pairs must be 0..7 (a bit mask)");
         g_heavy_pairs = (int)value;
         return SGC_OK;
     }
@@ -1456,13 +1600,24 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         // 32-bit row offsets (one full-rate 24-bit multiply per gathered row)
         // when the caller vouches that X spans < 4 GiB and has < 2^24 rows
         const bool o32 = (flags & SGC_SPMM_X_UNDER_4G) && ldx * 4 < (int64_t(1) << 24);
-#define SGC_ROWS(LBV, VHV)                                                     \
-    (o32 ? launch_rows<LBV, VHV, true>(a, (int)F4, LR, vec_store)              \
-         : launch_rows<LBV, VHV, false>(a, (int)F4, LR, vec_store))
-        if (LR >= 16)
-            e = vh2 ? SGC_ROWS(16, 2) : SGC_ROWS(16, 1);
+#define SGC_ROWS(LBV, VHV, QVV)                                                     \
+    (o32 ? launch_rows<LBV, VHV, true, QVV>(a, (int)F4, LR, vec_store)              \
+         : launch_rows<LBV, VHV, false, QVV>(a, (int)F4, LR, vec_store))
+        // heavy rows four nonzeros per load (row_quads_pipe) on launches of at
+        // most 32 floats; measured (one hop over all Reddit-shape rows,
+        // interleaved, bit-identical, profiles/r04/quads_ab.log) 32 floats
+        // 0.667 -> 0.615 ms, but 48 and 64 floats slower (0.68 -> 0.82, 0.72
+        // -> 0.85) and 64-float slices at full width far slower (3.8 -> 5.8):
+        // there the pairs stay
+        const int qv = ((g_heavy_pairs & 4) && LR <= 16 && F4 <= 32) ? (F4 > 16 ? 2 : 1) : 0;
+        if (qv == 2)
+            e = SGC_ROWS(8, 2, 2);
+        else if (qv == 1)
+            e = SGC_ROWS(8, 2, 1);
+        else if (LR >= 16)
+            e = vh2 ? SGC_ROWS(16, 2, 0) : SGC_ROWS(16, 1, 0);
         else
-            e = vh2 ? SGC_ROWS(8, 2) : SGC_ROWS(8, 1);
+            e = vh2 ? SGC_ROWS(8, 2, 0) : SGC_ROWS(8, 1, 0);
 #undef SGC_ROWS
     } else {
         const int V = pick_vec(F_csr, ldx, ldy, X, Y);

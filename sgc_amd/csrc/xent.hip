@@ -115,6 +115,8 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(
 }
 
 // ---- B: dW partial slabs -----------------------------------------------------
+constexpr int kDwDepth = 4;  // 4-row steps of G and X in flight per wave
+
 // Block blk reduces rows [blk*rows_per, ...) into slab[blk][C16][K].  Wave w
 // owns the K column groups {w, w+4, ...} of 16*V columns each.  MFMA k-step =
 // 4 rows: A[i=class][k=row] = G[row][class] (lane l: G[r0+(l>>4)][n*16+(l&15)]),
@@ -156,8 +158,8 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
         }
         // Columns past K read column 0 (finite) and are never stored; rows past
         // r_end only occur in the ragged last step, which zeroes their G.
-        float ga[NT], gn[NT];
-        VT xb[CT], xn[CT];
+        float ga[NT];  // the ragged tail's step
+        VT xb[CT];
         const bool sum_db = db_slab && gb == 0;  // wave 0, first column group: every row once
         float dba[NT];
 #pragma unroll
@@ -184,20 +186,27 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
                         acc[n][ct][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(
                             gd[n], lane_elem<V>(xd[ct], v), acc[n][ct][v], 0, 0, 0);
         };
+        // kDwDepth 4-row steps in flight (a ring of register buffers): the
+        // round-1 loop kept two and its waves sat 56 % of their cycles on
+        // s_waitcnt (profiles/r04/pmc_cls/sq.summary)
         const int n_full = (r_end - r_begin) / 4;
-        const int r_main = r_begin + 4 * n_full;
-        int r0 = r_begin;
-        if (n_full > 0) load(r0, ga, xb);
-        for (; r0 + 8 <= r_main; r0 += 8) {
-            load(r0 + 4, gn, xn);
-            mma(ga, xb);
-            if (r0 + 8 < r_main) load(r0 + 8, ga, xb);
-            mma(gn, xn);
+        float gr[kDwDepth][NT];
+        VT xr[kDwDepth][CT];
+#pragma unroll
+        for (int d = 0; d < kDwDepth; ++d)
+            if (d < n_full) load(r_begin + 4 * d, gr[d], xr[d]);
+        int s0 = 0;
+        for (; s0 + kDwDepth <= n_full; s0 += kDwDepth) {
+#pragma unroll
+            for (int d = 0; d < kDwDepth; ++d) {
+                mma(gr[d], xr[d]);
+                if (s0 + d + kDwDepth < n_full) load(r_begin + 4 * (s0 + d + kDwDepth), gr[d], xr[d]);
+            }
         }
-        if (r0 < r_main) {
-            mma(ga, xb);
-            r0 += 4;
-        }
+#pragma unroll
+        for (int d = 0; d < kDwDepth; ++d)  // the last n_full % kDwDepth steps, already loaded
+            if (s0 + d < n_full) mma(gr[d], xr[d]);
+        const int r0 = r_begin + 4 * n_full;
         if (r0 < r_end) {  // ragged tail: rows past r_end get G = 0
             const int r = r0 + g;
             const bool rok = r < r_end;

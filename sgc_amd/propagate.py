@@ -233,6 +233,24 @@ class DeviceCSR:
                                           self.status) for g in range(G)]
         return self._plans[key]
 
+    def drop_groups(self):
+        """Free the cached column-group copies of S (and their plans): one
+        more col/val copy per G (188 MB at Reddit shape).  They are rebuilt
+        on the next launch that uses them."""
+        for key in [k for k in self._plans if isinstance(k, tuple) and k[:1] == ("groups",)]:
+            for part in self._plans.pop(key):
+                part._plans.clear()
+
+    def groups_or_self(self, G):
+        """The G column-group CSRs, or [self] when G == 1 or when the copy
+        does not fit in device memory (a schedule: the results are the same)."""
+        if G <= 1:
+            return [self]
+        try:
+            return self.column_groups(G)
+        except torch.cuda.OutOfMemoryError:
+            return [self]
+
     @classmethod
     def from_host_arrays(cls, row_ptr, col_idx, val, n_cols=None, device="cuda"):
         """From host CSR arrays already in the SpMM's order (numpy or torch)."""
@@ -507,7 +525,7 @@ def spmm(csr: DeviceCSR, X: torch.Tensor, row_begin=0, row_end=None, out=None,
     G = 1
     if use_plan and not flags & (SPMM_ACCUMULATE | SPMM_NO_HUB | SPMM_HUB_ONLY):
         G = column_groups_for(csr, F)
-    parts = csr.column_groups(G) if G > 1 else [csr]
+    parts = csr.groups_or_self(G)
     with torch.cuda.device(X.device):
         stream = _lib.stream_handle(X.device)
         for g, c in enumerate(parts):  # group 0 plain, groups 1.. continue its chains
@@ -605,7 +623,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                                              _lib.ptr(out), out.stride(0), F, int(K), _lib.ptr(ws),
                                              ws_bytes, cpu_threads()), "propagate_f32_cpu")
         return out
-    G = column_groups_for(csr, F) if use_plan else 1
+    G = len(csr.groups_or_self(column_groups_for(csr, F) if use_plan else 1))
     if G > 1:
         pl = None
         parts = [(c, c.plan(0, n, threshold, hub_threshold, F)) for c in csr.column_groups(G)]

@@ -198,12 +198,21 @@ def test_bench_self_launch_two_ranks():
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--shape",
-           "pubmed", "--steps", "2", "--warmup", "1", "--alt-steps", "1", "--public-steps", "1"]
+           "pubmed", "--steps", "2", "--warmup", "1", "--sharded-steps", "1"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _last_json(r.stdout)
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["steps"] == 2
-    assert rec["public_call"]["value"] > 0 and "auto-selected" in rec["config"]["parallelism"]
+    # N > 1 times the same public call as N = 1 (replicated X_K) ...
+    assert rec["config"]["output"] == "replicated" and "sgc_precompute" in rec["timed_call"]
+    # ... with the roofline's kernel named by the library and a stated basis
+    roof = rec["roofline"]
+    assert roof["kernel"].startswith("spmm_") and roof["frac"] > 0
+    assert roof["compulsory_frac"] == roof["frac"] and "compulsory" in roof["achieved_basis"]
+    assert rec["first_call_seconds"] > 0
+    # the sharded partitioned path beside it, partition timed on the node
+    assert rec["sharded_output"]["value"] > 0
+    assert "auto-selected" in rec["sharded_output"]["parallelism"]
 
 
 # ---------------------------------------------------------------------------

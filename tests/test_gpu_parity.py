@@ -320,12 +320,27 @@ def test_long_hub_rows_bit_exact(oracle, F, hub_chunk, hub_loaders):
         lib.sgc_set_tuning(b"hub_loaders", 15)
 
 
-@pytest.mark.parametrize("F", [32, 36, 44, 76, 96, 100, 124, 152])
-def test_narrow_launches_rows_kernel(oracle, F):
+@pytest.mark.parametrize("heavy_pairs", [1, 5])
+@pytest.mark.parametrize("F", [1, 3, 4, 12, 16, 17, 30, 32, 33, 36, 44, 60, 64, 76, 96, 100, 124,
+                               152])
+def test_narrow_launches_rows_kernel(oracle, F, heavy_pairs):
     """Feature widths below a slice (the feature partition's column blocks,
     the row partition's narrow groups): spmm_rows_kernel packs 64 // (F/4)
     rows into a wave.  Heavy rows (threshold 40) and hub rows (500) on the
-    same launch; X in 128-B rows so hop 1 also takes 16-B lanes."""
+    same launch, heavy rows two nonzeros per load (heavy_pairs 1) or, up to
+    64 floats, four (5: row_quads_pipe with 4-, 2- or 1-float lanes); X in
+    128-B rows so hop 1 also takes 16-B lanes."""
+    from sgc_amd import _lib, graphs
+    from sgc_amd.propagate import DeviceCSR, propagate
+    lib = _lib.load()
+    _lib.check(lib.sgc_set_tuning(b"heavy_pairs", heavy_pairs), "set_tuning")
+    try:
+        _narrow_case(oracle, F)
+    finally:
+        lib.sgc_set_tuning(b"heavy_pairs", 5)
+
+
+def _narrow_case(oracle, F):
     from sgc_amd import graphs
     from sgc_amd.propagate import DeviceCSR, propagate
     rng = np.random.default_rng(F)
@@ -365,7 +380,7 @@ def _column_split(S, bounds):
     return out
 
 
-@pytest.mark.parametrize("F", [602, 256, 130, 64, 36])
+@pytest.mark.parametrize("F", [602, 256, 130, 64, 36, 30, 12])
 @pytest.mark.parametrize("rows_per_wave", [0, 1, 2])
 @pytest.mark.parametrize("th,hub", [(40, 500), (10**9, 10**9)])
 def test_accumulate_column_block_passes(oracle, F, rows_per_wave, th, hub):
