@@ -50,6 +50,10 @@ Also printed (same JSON line, N = 1):
                 cache-resident) and the compulsory model (S, X and Y once).
   shapes        the same measurement for the other BASELINE configs
                 (Cora-, Pubmed-, RMAT-shape), rank 0 at N = 1
+  classifier    the SGC classifier at Reddit-train shape (152,410 x 602 -> 41):
+                the MFMA forward and weight backward with bytes and frac, the
+                reference's training closure (drop-in SGC vs nn.Linear vs the
+                fused loss) and reddit.py's 2-step LBFGS (sgc_amd.classifier_bench)
   cpu_baseline  the reference's arithmetic as written -- torch.spmm(COO, X)
                 (utils.py:95), median of 3 hops on this host; plus torch CSR
                 and this library's own CPU twin at every available core
@@ -534,6 +538,8 @@ def main():
     ap.add_argument("--hops", type=int, default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-classifier", action="store_true",
+                    help="N=1: skip the classifier sub-record (forward / backward / closure / LBFGS)")
     ap.add_argument("--shapes", default="cora,pubmed,rmat",
                     help="N=1: other BASELINE configs measured into the same line "
                          "(comma list, or 'none')")
@@ -629,6 +635,12 @@ def main():
         if not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(S, X_host)
         del S, X_host
+        if not args.no_classifier:
+            # the classifier after the precompute (models.py:7-18) and the
+            # reference's training closure (reddit.py:51-64) at Reddit-train
+            # shape: MFMA forward, weight backward, closure, LBFGS
+            from sgc_amd.classifier_bench import classifier_record
+            rec["classifier"] = classifier_record(dev)
         subs = [s for s in args.shapes.split(",") if s and s != "none" and s != args.shape]
         if subs:
             rec["shapes"] = {}

@@ -237,6 +237,8 @@ class DeviceCSR:
         """Free the cached column-group copies of S (and their plans): one
         more col/val copy per G (188 MB at Reddit shape).  They are rebuilt
         on the next launch that uses them."""
+        for key in [k for k in self._plans if isinstance(k, tuple) and k[:1] == ("loop",)]:
+            del self._plans[key]  # prepared loops hold the groups' pointers
         for key in [k for k in self._plans if isinstance(k, tuple) and k[:1] == ("groups",)]:
             for part in self._plans.pop(key):
                 part._plans.clear()
@@ -623,7 +625,24 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                                              _lib.ptr(out), out.stride(0), F, int(K), _lib.ptr(ws),
                                              ws_bytes, cpu_threads()), "propagate_f32_cpu")
         return out
-    G = len(csr.groups_or_self(column_groups_for(csr, F) if use_plan else 1))
+    stream = _lib.stream_handle(X.device)
+    G_rule = column_groups_for(csr, F) if use_plan else 1
+    # small launches (Cora / Pubmed shape: 20-40 us hops) pay their host time:
+    # the Python loop's ctypes calls are prepared once per (X, out, K, stream,
+    # schedule) and replayed, with the intermediates kept with them
+    key = None
+    if not native_loop and hop_hook is None:
+        key = ("loop", X.data_ptr(), X.stride(0), F, int(K), out.data_ptr(), out.stride(0),
+               threshold, hub_threshold, bool(use_plan), G_rule, stream.value)
+        prep = csr._plans.get(key)
+        if prep is not None:
+            with torch.cuda.device(X.device):
+                for fn, args in prep[1]:
+                    rc = fn(*args)
+                    if rc:
+                        _lib.check(rc, "propagate (prepared)")
+            return out
+    G = len(csr.groups_or_self(G_rule))
     if G > 1:
         pl = None
         parts = [(c, c.plan(0, n, threshold, hub_threshold, F)) for c in csr.column_groups(G)]
@@ -633,7 +652,6 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
     # (csr, plan, launch flags of the group): groups 1.. continue group 0's chains
     parts = [(c, cp, cp.hub_flags() | (SPMM_ACCUMULATE if g else 0))
              for g, (c, cp) in enumerate(parts)]
-    stream = _lib.stream_handle(X.device)
     ldw = aligned_ld(F)
     with torch.cuda.device(X.device):
         if native_loop:  # the same loop inside one C ABI call (sgc_propagate_groups_f32)
@@ -661,13 +679,16 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
         # buffers actually used: the re-laid X_0 (if any) + up to two
         # ping-pong intermediates (the last hop writes `out`)
         n_bufs = min(2, int(pad) + min(K - 1, 2))
+        prepared = key is not None and n_bufs * n * ldw * 4 <= PREPARED_LOOP_MAX_BYTES
         bufs = [torch.empty((n, ldw), dtype=torch.float32, device=X.device)
                 for _ in range(n_bufs)]
+        launches = []  # (fn, args) of the loop, in order
         src, nxt = X, 0
         if pad:
-            _lib.check(lib.sgc_pad_rows_f32(_lib.ptr(X), X.stride(0), _lib.ptr(bufs[0]), ldw, n, F,
-                                            stream), "pad_rows_f32")
+            launches.append((lib.sgc_pad_rows_f32, (_lib.ptr(X), X.stride(0), _lib.ptr(bufs[0]),
+                                                    ldw, n, F, stream)))
             src, nxt = bufs[0][:, :F], 1 % len(bufs)
+            _lib.check(launches[-1][0](*launches[-1][1]), "pad_rows_f32")
         for h in range(K):
             dst = out if h == K - 1 else bufs[nxt][:, :F]
             # the engine's own buffers may be read / written in their pad columns
@@ -676,16 +697,27 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
             if hop_hook:
                 hop_hook("start", h)
             for c, cp, gflags in parts:  # column groups: 0 plain, 1.. accumulate
-                _lib.check(lib.sgc_spmm_csr_f32_ex(_lib.ptr(c.row_ptr), _lib.ptr(c.col_idx),
-                                                   _lib.ptr(c.val), 0, n, _lib.ptr(src),
-                                                   src.stride(0), _lib.ptr(dst), dst.stride(0),
-                                                   F, _lib.ptr(cp.rows), cp.n_heavy, cp.n_hub,
-                                                   cp.threshold, flags | gflags, stream),
-                           "spmm_csr_f32")
+                args = (_lib.ptr(c.row_ptr), _lib.ptr(c.col_idx), _lib.ptr(c.val), 0, n,
+                        _lib.ptr(src), src.stride(0), _lib.ptr(dst), dst.stride(0), F,
+                        _lib.ptr(cp.rows), cp.n_heavy, cp.n_hub, cp.threshold, flags | gflags,
+                        stream)
+                launches.append((lib.sgc_spmm_csr_f32_ex, args))
+                _lib.check(lib.sgc_spmm_csr_f32_ex(*args), "spmm_csr_f32")
             if hop_hook:
                 hop_hook("end", h)
             src, nxt = dst, nxt ^ 1
+        if prepared:
+            old = [k for k in csr._plans if isinstance(k, tuple) and k[:1] == ("loop",)]
+            for k in old[:max(0, len(old) - PREPARED_LOOPS_KEPT + 1)]:
+                del csr._plans[k]  # oldest first (dicts keep insertion order)
+            csr._plans[key] = (bufs, launches, parts)  # parts: keep the pointers alive
     return out
+
+
+# propagate()'s prepared loops: at most this many bytes of intermediates each,
+# and this many (X, out, K, stream) combinations per adjacency
+PREPARED_LOOP_MAX_BYTES = 1 << 26
+PREPARED_LOOPS_KEPT = 4
 
 
 class GraphedPropagation:

@@ -639,6 +639,30 @@ def test_graphed_propagation_bit_exact(tiny_cases, name, K, hub):
         g.run(X[:, :1].contiguous())
 
 
+@pytest.mark.parametrize("name,K", [("norm_n48_F602", 3), ("hub1000_F130", 2), ("norm_n48_F65", 1)])
+def test_prepared_loop_replay_bit_exact(tiny_cases, name, K):
+    """propagate()'s prepared loop (second call with the same X / out / K):
+    the reference's bits, new contents of X picked up, a hop_hook call (the
+    unprepared loop) agreeing, and drop_groups() dropping the prepared loops."""
+    from sgc_amd.propagate import DeviceCSR, propagate
+    c = tiny_cases[name]
+    csr = DeviceCSR.from_torch(coo_cuda(c))
+    X = torch.from_numpy(c["X"]).to(DEV)
+    out = torch.full_like(X, float("nan"))
+    for _ in range(2):
+        propagate(csr, X, K, out=out)
+        torch.cuda.synchronize()
+        assert bits_equal(out.cpu().numpy(), c[f"Y{K}"])
+    assert any(isinstance(k, tuple) and k[0] == "loop" for k in csr._plans)
+    X.copy_(torch.flip(X, dims=[0]))
+    want = propagate(csr, X, K, hop_hook=lambda *a: None).cpu().numpy()
+    propagate(csr, X, K, out=out)
+    torch.cuda.synchronize()
+    assert bits_equal(out.cpu().numpy(), want)
+    csr.drop_groups()
+    assert not any(isinstance(k, tuple) and k[0] == "loop" for k in csr._plans)
+
+
 @pytest.mark.parametrize("r0,r1,th", [(0, 4000, 7), (123, 3001, 0), (0, 4000, 2**31 - 1), (50, 50, 5)])
 def test_plan_light_order(r0, r1, th):
     """sgc_plan_light_order: the light rows (degree <= threshold) of the range,
