@@ -146,8 +146,16 @@ def main():
     ap.add_argument("--classes", type=int, default=41)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--workload", action="store_true", help="kernels only (profiling)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="sgc_set_tuning before timing (e.g. tile_buffers=1)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if a.tune:
+        from . import _lib
+        lib = _lib.load()
+        for kv in a.tune:
+            k, v = kv.split("=")
+            _lib.check(lib.sgc_set_tuning(k.encode(), int(v)), "set_tuning")
     if a.workload:
         workload(dev, a.rows, a.features, a.classes)
         return

@@ -57,6 +57,10 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 
 // V consecutive fp32 in one lane: float / float2 / float4 register vectors,
 // loaded with one global_load_dword{,x2,x4}.
+// LDS image depth of the classifier tile (gemm_tile.h; linear.hip defines it,
+// sgc_set_tuning("tile_buffers") sets it: 1 or 2).
+extern int g_tile_buffers;
+
 template <int V> struct Vec { typedef float __attribute__((ext_vector_type(V))) T; };
 template <> struct Vec<1> { typedef float T; };
 

@@ -14,18 +14,18 @@
 
 namespace sgc {
 
-template <int V, int NT>
+template <int V, int NT, int NB>
 __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ X, int64_t ldx,
                                                      const float *__restrict__ W,
                                                      const float *__restrict__ b,
                                                      float *__restrict__ Y, int64_t ldy, int M,
                                                      int K, int C) {
-    __shared__ LdsTile<V, NT> sm;
+    __shared__ LdsTile<V, NT, NB> sm;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = lane & 15, g = lane >> 4;
     const int m_blk = blockIdx.x * kLdsBM;
     f32x4 acc[2][NT];
-    xwt_block_tile<V, NT>(X, ldx, W, M, K, C, m_blk, sm, acc);
+    xwt_block_tile<V, NT, NB>(X, ldx, W, M, K, C, m_blk, sm, acc);
     const int m0 = m_blk + w * 32;
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
@@ -42,14 +42,20 @@ __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ X
     }
 }
 
+int g_tile_buffers = 2;
+
 namespace {
 
 template <int V, int NT>
 hipError_t launch_linear(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                          int64_t ldy, int M, int K, int C, hipStream_t s) {
     const int64_t blocks = (M + kLdsBM - 1) / kLdsBM;
-    hipLaunchKernelGGL((linear_kernel<V, NT>), dim3((unsigned)blocks), dim3(256), 0, s, X, ldx, W,
-                       b, Y, ldy, M, K, C);
+    if (g_tile_buffers == 1)
+        hipLaunchKernelGGL((linear_kernel<V, NT, 1>), dim3((unsigned)blocks), dim3(256), 0, s, X,
+                           ldx, W, b, Y, ldy, M, K, C);
+    else
+        hipLaunchKernelGGL((linear_kernel<V, NT, 2>), dim3((unsigned)blocks), dim3(256), 0, s, X,
+                           ldx, W, b, Y, ldy, M, K, C);
     return hipGetLastError();
 }
 
@@ -74,6 +80,9 @@ int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *
                 "linear: bad shape M=%lld K=%lld C=%lld ldx=%lld ldy=%lld", (long long)M,
                 (long long)K, (long long)C, (long long)ldx, (long long)ldy);
     SGC_REQUIRE(M < INT32_MAX && K < INT32_MAX, SGC_ERANGE, "linear: too large");
+    SGC_REQUIRE(block_tile_fits(ldx, K, std::min<int64_t>(C, 64)), SGC_ERANGE,
+                "linear: ldx=%lld / K=%lld past the tile's 31-bit offsets", (long long)ldx,
+                (long long)K);
     if (M == 0) return SGC_OK;
     // classes are processed 64 at a time (NT <= 4 tiles of 16)
     for (int64_t c0 = 0; c0 < C; c0 += 64) {
@@ -84,6 +93,7 @@ int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *
         float *Yc = Y + c0;
         int V = 1;
         for (int v : {4, 2}) {
+            // natural alignment of every vector load (the k >= K tail is masked)
             if (K % v == 0 && ldx % v == 0 && reinterpret_cast<uintptr_t>(X) % (4 * v) == 0 &&
                 reinterpret_cast<uintptr_t>(Wc) % (4 * v) == 0) {
                 V = v;

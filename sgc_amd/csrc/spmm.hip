@@ -1422,6 +1422,11 @@ int set_tuning(const char *key, int64_t value) {
         g_heavy_pairs = (int)value;
         return SGC_OK;
     }
+    if (std::string(key) == "tile_buffers") {
+        SGC_REQUIRE(value == 1 || value == 2, SGC_EINVAL, "tile_buffers must be 1 or 2");
+        g_tile_buffers = (int)value;
+        return SGC_OK;
+    }
     if (std::string(key) == "max_vec") {
         SGC_REQUIRE(value == 1 || value == 2 || value == 4, SGC_EINVAL, "max_vec must be 1, 2 or 4");
         g_max_vec = (int)value;
@@ -1439,6 +1444,7 @@ int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
     if (key && std::string(key) == "hub_stream") return g_hub_stream;
     if (key && std::string(key) == "hub_loaders") return g_hub_loaders;
+    if (key && std::string(key) == "tile_buffers") return g_tile_buffers;
     return -1;
 }
 

@@ -35,13 +35,13 @@ __device__ __forceinline__ float group16_sum(float v) {
 }
 
 // ---- A: logits -> G, loss / dG partials ------------------------------------
-template <int V, int NT>
+template <int V, int NT, int NB>
 __global__ __launch_bounds__(256) void xent_fwd_kernel(
     const float *__restrict__ X, int64_t ldx, const float *__restrict__ W,
     const float *__restrict__ b, const int64_t *__restrict__ labels, int M, int K, int C,
     float inv_m, float *__restrict__ G, int ldg, double *__restrict__ loss_part,
     float *__restrict__ db_part, float *__restrict__ logits, int64_t ldl) {
-    __shared__ LdsTile<V, NT> sm;
+    __shared__ LdsTile<V, NT, NB> sm;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int wave = blockIdx.x * 4 + w;
     const int i = lane & 15, g = lane >> 4;
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(
     for (int n = 0; n < NT; ++n) dbc[n] = 0.f;
     {
         f32x4 acc[2][NT];
-        xwt_block_tile<V, NT>(X, ldx, W, M, K, C, m_blk, sm, acc);
+        xwt_block_tile<V, NT, NB>(X, ldx, W, M, K, C, m_blk, sm, acc);
         float bias[NT];
         bool valid[NT];
 #pragma unroll
@@ -117,6 +117,11 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(
 // ---- B: dW partial slabs -----------------------------------------------------
 constexpr int kDwDepth = 4;  // 4-row steps of G and X in flight per wave
 
+// Host-side precondition of xent_dw_kernel's buffer offsets.
+inline bool dw_slab_fits(int64_t rows_per, int64_t ldx, int64_t ldg) {
+    return (rows_per + 4) * std::max(ldx, ldg) * 4 < (int64_t(1) << 31);
+}
+
 // Block blk reduces rows [blk*rows_per, ...) into slab[blk][C16][K].  Wave w
 // owns the K column groups {w, w+4, ...} of 16*V columns each.  MFMA k-step =
 // 4 rows: A[i=class][k=row] = G[row][class] (lane l: G[r0+(l>>4)][n*16+(l&15)]),
@@ -156,21 +161,38 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
             cok[ct] = c < K;
             coff[ct] = cok[ct] ? c : 0;
         }
-        // Columns past K read column 0 (finite) and are never stored; rows past
-        // r_end only occur in the ragged last step, which zeroes their G.
-        float ga[NT];  // the ragged tail's step
-        VT xb[CT];
+        // Buffer loads (round 4): one descriptor for the block's rows of X and
+        // one for its rows of G, each lane's byte offset computed once and the
+        // step's row offset a scalar, so a load costs one add.  Rows past
+        // r_end lie outside both descriptors (zeros: the ragged last step
+        // needs no code of its own) and so do classes >= C.  Columns past K
+        // read column 0 (finite) and are never stored.
+        const int n_rows = max(0, r_end - r_begin);  // 0: an empty trailing block
+        const auto xdsc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float *>(X + (int64_t)r_begin * ldx), 0,
+            n_rows ? (int)(((int64_t)(n_rows - 1) * ldx + K) * 4) : 0, 0x00020000);
+        const auto gdsc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float *>(G + (int64_t)r_begin * ldg), 0,
+            n_rows ? (int)(((int64_t)(n_rows - 1) * ldg + C) * 4) : 0, 0x00020000);
+        uint32_t xo[CT], go[NT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) xo[ct] = (uint32_t)(g * ldx + coff[ct]) * 4u;
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+            go[n] = (n * 16 + i < C) ? (uint32_t)(g * ldg + n * 16 + i) * 4u : kOffOOB;
         const bool sum_db = db_slab && gb == 0;  // wave 0, first column group: every row once
         float dba[NT];
 #pragma unroll
         for (int n = 0; n < NT; ++n) dba[n] = 0.f;
-        auto load = [&](int r0, float (&gd)[NT], VT (&xd)[CT]) {
-            const int64_t r = r0 + g;
+        auto load = [&](int step, float (&gd)[NT], VT (&xd)[CT]) {
+            const uint32_t rx = (uint32_t)(4 * step) * (uint32_t)ldx * 4u;
+            const uint32_t rg = (uint32_t)(4 * step) * (uint32_t)ldg * 4u;
 #pragma unroll
-            for (int n = 0; n < NT; ++n) gd[n] = (n * 16 + i < C) ? G[r * ldg + n * 16 + i] : 0.f;
-            const float *xr = X + r * ldx;
+            for (int n = 0; n < NT; ++n)
+                gd[n] = __builtin_bit_cast(float,
+                                           __builtin_amdgcn_raw_buffer_load_b32(gdsc, go[n] + rg, 0, 0));
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct) xd[ct] = *reinterpret_cast<const VT *>(xr + coff[ct]);
+            for (int ct = 0; ct < CT; ++ct) xd[ct] = buffer_load_vec<V>(xdsc, xo[ct] + rx);
         };
         auto mma = [&](const float (&gd)[NT], const VT (&xd)[CT]) {
             if (sum_db) {
@@ -189,35 +211,23 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
         // kDwDepth 4-row steps in flight (a ring of register buffers): the
         // round-1 loop kept two and its waves sat 56 % of their cycles on
         // s_waitcnt (profiles/r04/pmc_cls/sq.summary)
-        const int n_full = (r_end - r_begin) / 4;
+        const int n_steps = (n_rows + 3) / 4;
         float gr[kDwDepth][NT];
         VT xr[kDwDepth][CT];
 #pragma unroll
         for (int d = 0; d < kDwDepth; ++d)
-            if (d < n_full) load(r_begin + 4 * d, gr[d], xr[d]);
+            if (d < n_steps) load(d, gr[d], xr[d]);
         int s0 = 0;
-        for (; s0 + kDwDepth <= n_full; s0 += kDwDepth) {
+        for (; s0 + kDwDepth <= n_steps; s0 += kDwDepth) {
 #pragma unroll
             for (int d = 0; d < kDwDepth; ++d) {
                 mma(gr[d], xr[d]);
-                if (s0 + d + kDwDepth < n_full) load(r_begin + 4 * (s0 + d + kDwDepth), gr[d], xr[d]);
+                if (s0 + d + kDwDepth < n_steps) load(s0 + d + kDwDepth, gr[d], xr[d]);
             }
         }
 #pragma unroll
-        for (int d = 0; d < kDwDepth; ++d)  // the last n_full % kDwDepth steps, already loaded
-            if (s0 + d < n_full) mma(gr[d], xr[d]);
-        const int r0 = r_begin + 4 * n_full;
-        if (r0 < r_end) {  // ragged tail: rows past r_end get G = 0
-            const int r = r0 + g;
-            const bool rok = r < r_end;
-            const int64_t rr = rok ? r : r_begin;
-#pragma unroll
-            for (int n = 0; n < NT; ++n) ga[n] = (rok && n * 16 + i < C) ? G[rr * ldg + n * 16 + i] : 0.f;
-            const float *xr = X + rr * ldx;
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) xb[ct] = *reinterpret_cast<const VT *>(xr + coff[ct]);
-            mma(ga, xb);
-        }
+        for (int d = 0; d < kDwDepth; ++d)  // the last n_steps % kDwDepth steps, already loaded
+            if (s0 + d < n_steps) mma(gr[d], xr[d]);
         if (sum_db) {
 #pragma unroll
             for (int n = 0; n < NT; ++n) {
@@ -312,8 +322,14 @@ hipError_t launch_fwd(const float *X, int64_t ldx, const float *W, const float *
                       double *loss_part, float *db_part, float *logits, int64_t ldl,
                       hipStream_t s) {
     const int blocks = (M + kLdsBM - 1) / kLdsBM;
-    hipLaunchKernelGGL((xent_fwd_kernel<V, NT>), dim3(blocks), dim3(256), 0, s, X, ldx, W, b,
-                       labels, M, K, C, 1.0f / (float)M, G, ldg, loss_part, db_part, logits, ldl);
+    if (g_tile_buffers == 1)
+        hipLaunchKernelGGL((xent_fwd_kernel<V, NT, 1>), dim3(blocks), dim3(256), 0, s, X, ldx, W,
+                           b, labels, M, K, C, 1.0f / (float)M, G, ldg, loss_part, db_part, logits,
+                           ldl);
+    else
+        hipLaunchKernelGGL((xent_fwd_kernel<V, NT, 2>), dim3(blocks), dim3(256), 0, s, X, ldx, W,
+                           b, labels, M, K, C, 1.0f / (float)M, G, ldg, loss_part, db_part, logits,
+                           ldl);
     return hipGetLastError();
 }
 
@@ -347,6 +363,9 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
                 (long long)K, (long long)C);
     SGC_REQUIRE(M < INT32_MAX && K < INT32_MAX, SGC_ERANGE, "linear_xent: too large");
     SGC_REQUIRE(!logits || ldl >= C, SGC_EINVAL, "linear_xent: ldl < C");
+    SGC_REQUIRE(block_tile_fits(ldx, K, C), SGC_ERANGE,
+                "linear_xent: ldx=%lld / K=%lld past the tile's 31-bit offsets", (long long)ldx,
+                (long long)K);
     const int64_t need = xent_workspace_bytes(M, K, C);
     SGC_REQUIRE(ws_bytes >= need, SGC_ENOMEM, "linear_xent: workspace %lld < %lld",
                 (long long)ws_bytes, (long long)need);
@@ -355,6 +374,9 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
     const int waves = (int)((M + kLdsBM - 1) / kLdsBM * 4);
     const int n_slabs = (int)std::min<int64_t>(512, (M + 255) / 256);
     const int rows_per = (int)(((M + n_slabs - 1) / n_slabs + 3) / 4 * 4);
+    SGC_REQUIRE(dw_slab_fits(rows_per, ldx, NT * 16), SGC_ERANGE,
+                "classifier dW: %d rows x ldx %lld past the kernel's 31-bit offsets", rows_per,
+                (long long)ldx);
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     char *p = (char *)(((uintptr_t)ws + 255) & ~uintptr_t(255));
     float *G = (float *)p;
@@ -444,6 +466,9 @@ int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ld
     const int C16 = NT * 16;
     const int n_slabs = (int)std::min<int64_t>(512, (M + 255) / 256);
     const int rows_per = (int)(((M + n_slabs - 1) / n_slabs + 3) / 4 * 4);
+    SGC_REQUIRE(dw_slab_fits(rows_per, ldx, ldd), SGC_ERANGE,
+                "classifier dW: %d rows x ldx %lld past the kernel's 31-bit offsets", rows_per,
+                (long long)ldx);
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     char *p = (char *)(((uintptr_t)ws + 255) & ~uintptr_t(255));
     float *slab = (float *)p;

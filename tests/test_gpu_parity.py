@@ -522,6 +522,37 @@ def test_linear_mfma_vs_torch_fp32(M, K, C):
     torch.testing.assert_close(Yn, ref - b, rtol=1e-5, atol=tol)
 
 
+@pytest.mark.parametrize("tile_buffers", [1, 2])
+@pytest.mark.parametrize("M,K,C,ld_extra", [(129, 602, 41, 6), (300, 33, 17, 0), (257, 31, 3, 1),
+                                            (128, 64, 64, 32), (1, 1, 1, 3), (500, 602, 70, 2)])
+def test_linear_tile_edges(tile_buffers, M, K, C, ld_extra):
+    """The classifier tile's buffer loads (gemm_tile.h): rows past M, classes
+    past C and the k >= K tail of the last chunk read as zeros -- X's columns
+    past K hold infinities here, so an unmasked tail would give NaN -- with one
+    or two LDS images; forward and the fused step's logits."""
+    from sgc_amd import _lib
+    from sgc_amd.propagate import linear, linear_xent
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + K + C)
+    Xf = torch.full((M, K + ld_extra), float("inf"))
+    Xf[:, :K] = torch.randn((M, K), generator=g)
+    W = torch.randn((C, K), generator=g) * 0.05
+    b = torch.randn(C, generator=g)
+    y = torch.randint(0, C, (M,), generator=g)
+    ref = torch.nn.functional.linear(Xf[:, :K].double(), W.double(), b.double())
+    tol = 1e-5 * max(1.0, ref.abs().max().item())
+    _lib.check(lib.sgc_set_tuning(b"tile_buffers", tile_buffers), "set_tuning")
+    try:
+        Xd = Xf.to(DEV)[:, :K]
+        Y = linear(Xd, W.to(DEV), b.to(DEV)).cpu().double()
+        torch.testing.assert_close(Y, ref, rtol=1e-5, atol=tol)
+        if C <= 64:
+            _, _, _, logits = linear_xent(Xd, W.to(DEV), b.to(DEV), y.to(DEV), want_logits=True)
+            torch.testing.assert_close(logits.cpu().double(), ref, rtol=1e-5, atol=tol)
+    finally:
+        lib.sgc_set_tuning(b"tile_buffers", 2)
+
+
 def test_sgc_model_autograd_matches_torch():
     from sgc_amd.models import SGC, get_model
     torch.manual_seed(0)
