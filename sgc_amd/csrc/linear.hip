@@ -42,7 +42,10 @@ __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ X
     }
 }
 
-int g_tile_buffers = 2;
+// One LDS image per block (two barriers per chunk, half the LDS: twice the
+// blocks per CU) measured faster than the double buffer at the Reddit-train
+// shape: forward 0.128-0.130 vs 0.146-0.152 ms (profiles/r04/classifier_v3_*.log).
+int g_tile_buffers = 1;
 
 namespace {
 

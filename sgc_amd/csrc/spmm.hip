@@ -270,7 +270,14 @@ constexpr int kPairsU = 4;  // nonzero pairs per step (8 nonzeros; 16 in flight)
 // did), the last block stops at the row's end; the (col, val) block after
 // next is loaded before the gathers of the step that starts the next block.
 // Reddit shape K=2: 9.01 -> 8.94 ms, bit-identical (profiles/r03/s5/pairs.log).
-template <int U, bool O32>
+//
+// TR (transposed pairs, heavy_pairs bit 16): one v_permlane32_swap per two
+// registers instead -- (r0, r2) and (r1, r3) -- leaves lane (h, j) (h = lane
+// >= 32) with features 4j+2h, 4j+2h+1 of both nonzeros, so each lane runs
+// two chains (its two features) at one FMA per nonzero each: two swaps and
+// four FMAs per pair where the untransposed form spends four and eight (both
+// halves computing every chain); every lane stores its two features.
+template <int U, bool O32, bool TR = false>
 __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
                                                const float *__restrict__ val, int k0, int k1,
                                                const float *__restrict__ X, int64_t ldx,
@@ -281,11 +288,22 @@ __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
     constexpr int kPairs = kWave / (2 * U);  // steps per 64-nonzero block
     static_assert(kWave % (2 * U) == 0 && kPairs % 2 == 0, "2U must divide 64 into an even count");
     if (accum && k1 == k0) return;
+    typedef float f2 __attribute__((ext_vector_type(2)));
     const bool hi = lane >= 32;
     const uint32_t boff = lane_ok ? uint32_t(f_lane) * 4u : 0u;
     f4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    f2 acc2 = {0.0f, 0.0f};           // TR: features fo, fo + 1
+    const int fo = f_lane + (hi ? 2 : 0);
     if (accum && lane_ok) {
-        if (vec_store) {
+        if constexpr (TR) {
+            if (vec_store) {
+                acc2 = *reinterpret_cast<const f2 *>(yrow + fo);
+            } else {
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+                    if (fo + v < F) acc2[v] = yrow[fo + v];
+            }
+        } else if (vec_store) {
             acc = *reinterpret_cast<const f4 *>(yrow + f_lane);
         } else {
 #pragma unroll
@@ -339,6 +357,20 @@ __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
             for (int u = 0; u < U; ++u) {
                 const int ka = cur + 2 * u;
                 if (ka > last) break;  // uniform
+                if constexpr (TR) {
+                    const f4 x = xv[i & 1][u];
+                    const auto s02 = __builtin_amdgcn_permlane32_swap(
+                        __float_as_uint(x[0]), __float_as_uint(x[2]), false, false);
+                    const auto s13 = __builtin_amdgcn_permlane32_swap(
+                        __float_as_uint(x[1]), __float_as_uint(x[3]), false, false);
+                    acc2[0] = __builtin_fmaf(v0[i & 1][u], __uint_as_float(s02[0]), acc2[0]);
+                    acc2[1] = __builtin_fmaf(v0[i & 1][u], __uint_as_float(s13[0]), acc2[1]);
+                    if (ka + 1 <= last) {
+                        acc2[0] = __builtin_fmaf(v1[i & 1][u], __uint_as_float(s02[1]), acc2[0]);
+                        acc2[1] = __builtin_fmaf(v1[i & 1][u], __uint_as_float(s13[1]), acc2[1]);
+                    }
+                    continue;
+                }
                 f4 xa, xb;
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
@@ -367,7 +399,17 @@ __device__ __forceinline__ void row_pairs_pipe(const int *__restrict__ col,
         for (int i = 0; i < kPairs; ++i)  // no exit: skipped steps fall through
             if (base + i * 2 * U <= last) step(base, i, true);
     }
-    if (!hi && lane_ok) {
+    if constexpr (TR) {
+        if (lane_ok) {
+            if (vec_store) {
+                *reinterpret_cast<f2 *>(yrow + fo) = acc2;
+            } else {
+#pragma unroll
+                for (int v = 0; v < 2; ++v)
+                    if (fo + v < F) yrow[fo + v] = acc2[v];
+            }
+        }
+    } else if (!hi && lane_ok) {
         if (vec_store) {
             *reinterpret_cast<f4 *>(yrow + f_lane) = acc;
         } else {
@@ -512,6 +554,114 @@ __device__ __forceinline__ void row_quads_pipe(const int *__restrict__ col,
     }
 }
 
+// Heavy row of a 33..64-float launch, four nonzeros per load, TRANSPOSED: lane
+// (g, j) (g = lane / 16, j = lane & 15) gathers floats 4j..4j+3 of nonzero
+// k+g's segment -- one load moves four 256-B segments, as the light rows' do
+// at this width -- and then a 4 x 4 transpose across the four lane groups
+// (two v_permlane32_swap: g <-> g^2, two v_permlane16_swap: g <-> g^1) leaves
+// lane (g, j) with feature 4j+g of the four nonzeros, in nonzero order:
+//   after the 32-swaps (r0,r2), (r1,r3): g < 2 holds f0,f1 of nonzeros g, g+2;
+//     g >= 2 holds f2,f3 of nonzeros g-2, g;
+//   after the 16-swaps (r0,r1), (r2,r3): r0..r3 = feature 4j+g of nonzeros
+//     k..k+3.
+// Each lane then runs ONE chain (its feature) with one FMA per nonzero:
+// four swaps + four FMAs per four nonzeros, where row_quads_pipe at V = 4
+// spends twelve permutes and sixteen FMAs (every group recomputing every
+// chain) -- the reason it lost to the pairs at 48-64 floats.  The chain is
+// the same sequential fmaf chain per element; every lane stores its feature.
+template <int U, bool O32>
+__device__ __forceinline__ void row_quadsT_pipe(const int *__restrict__ col,
+                                                const float *__restrict__ val, int k0, int k1,
+                                                const float *__restrict__ X, int64_t ldx,
+                                                float *__restrict__ yrow, int F, int f_lane,
+                                                bool lane_ok, int lane, bool accum) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    constexpr int kSteps = kWave / (4 * U);  // steps per 64-nonzero block
+    static_assert(kWave % (4 * U) == 0 && kSteps % 2 == 0, "4U must divide 64 into an even count");
+    if (accum && k1 == k0) return;
+    const int g = lane >> 4;
+    const int fo = f_lane + g;  // this lane's output feature
+    const bool own = lane_ok && fo < F;
+    const uint32_t boff = lane_ok ? uint32_t(f_lane) * 4u : 0u;
+    float acc = 0.0f;
+    if (accum && own) acc = yrow[fo];
+    if (k1 > k0) {
+        const char *Xb = reinterpret_cast<const char *>(X);
+        const int64_t row_bytes = ldx * 4;
+        const int last = k1 - 1;
+        int colA = ld_meta(col + min(k0 + lane, last));
+        float valA = ld_meta(val + min(k0 + lane, last));
+        int colB = ld_meta(col + min(k0 + kWave + lane, last));
+        float valB = ld_meta(val + min(k0 + kWave + lane, last));
+        f4 xv[2][U];
+        float vq[2][U][4];
+        auto issue = [&](int base, int i, int colr, float valr, int buf) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int kq = base + i * 4 * U + 4 * u;
+                int c[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int l = (min(kq + j, last) - base) & (kWave - 1);
+                    c[j] = __builtin_amdgcn_readlane(colr, l);
+                    vq[buf][u][j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(valr), l));
+                }
+                const int c01 = (g & 1) ? c[1] : c[0];
+                const int c23 = (g & 1) ? c[3] : c[2];
+                const int cj = (g & 2) ? c23 : c01;
+                if constexpr (O32)
+                    xv[buf][u] = *reinterpret_cast<const f4 *>(
+                        Xb + (__umul24((uint32_t)cj, (uint32_t)row_bytes) + boff));
+                else
+                    xv[buf][u] = *reinterpret_cast<const f4 *>(Xb + (int64_t)cj * row_bytes + boff);
+            }
+        };
+        auto step = [&](int base, int i, bool last_block) {
+            const int cur = base + i * 4 * U;
+            if (i + 1 < kSteps) {
+                issue(base, i + 1, colA, valA, (i + 1) & 1);
+            } else if (!last_block) {
+                const int nb2 = base + 2 * kWave;  // the block after next
+                const int cN = ld_meta(col + min(nb2 + lane, last));
+                const float vN = ld_meta(val + min(nb2 + lane, last));
+                issue(base + kWave, 0, colB, valB, 0);
+                colA = colB;
+                valA = valB;
+                colB = cN;
+                valB = vN;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int kq = cur + 4 * u;
+                if (kq > last) break;  // uniform
+                const int n_here = min(4, last - kq + 1);  // uniform
+                const f4 x = xv[i & 1][u];
+                const auto s02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[0]),
+                                                                  __float_as_uint(x[2]), false, false);
+                const auto s13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[1]),
+                                                                  __float_as_uint(x[3]), false, false);
+                const auto t01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);
+                const auto t23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);
+                acc = __builtin_fmaf(vq[i & 1][u][0], __uint_as_float(t01[0]), acc);
+                if (n_here > 1) acc = __builtin_fmaf(vq[i & 1][u][1], __uint_as_float(t01[1]), acc);
+                if (n_here > 2) acc = __builtin_fmaf(vq[i & 1][u][2], __uint_as_float(t23[0]), acc);
+                if (n_here > 3) acc = __builtin_fmaf(vq[i & 1][u][3], __uint_as_float(t23[1]), acc);
+            }
+        };
+        issue(k0, 0, colA, valA, 0);
+        const int nblk = (k1 - k0 + kWave - 1) / kWave;
+        int base = k0;
+        for (int b = 0; b + 1 < nblk; ++b, base += kWave) {
+#pragma unroll
+            for (int i = 0; i < kSteps; ++i) step(base, i, false);
+        }
+#pragma unroll
+        for (int i = 0; i < kSteps; ++i)  // no exit: skipped steps fall through
+            if (base + i * 4 * U <= last) step(base, i, true);
+    }
+    if (own) yrow[fo] = acc;
+}
+
 // Grid: x = work items of one feature slice, y = slice.  Workgroups are
 // dispatched x-fastest, so the chip sweeps the slices one after another and
 // only X[:, slice] (N x 64CV floats -- 119 MB at Reddit shape for 128
@@ -626,7 +776,13 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
         const int h = wave / n_sub;
         const int row = heavy_rows[h];
         const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
-        if constexpr (QV > 0) {  // 16 lanes per row: four nonzeros per load
+        if constexpr (QV == 4) {  // 16 lanes x 16 B per nonzero, transposed chains
+            const int f = slice * (LR * V) + (lane & 15) * 4;
+            row_quadsT_pipe<kQuadsU, O32>(col, val, k0, k1, X, ldx,
+                                          Y + (int64_t)(row - row_begin) * ldy, F, f, f < F_load,
+                                          lane, accum != 0);
+            return;
+        } else if constexpr (QV > 0) {  // 16 lanes per row: four nonzeros per load
             const int f = slice * (LR * V) + (lane & 15) * QV;
             row_quads_pipe<QV, kQuadsU, O32>(col, val, k0, k1, X, ldx,
                                              Y + (int64_t)(row - row_begin) * ldy, F, f,
@@ -636,9 +792,15 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
         if (heavy_pairs & 1) {  // n_sub == 1: one item per (row, slice), two nonzeros per load
             const int j = lane & 31;
             const int f = slice * (LR * V) + j * V;
-            row_pairs_pipe<kPairsU, O32>(col, val, k0, k1, X, ldx,
-                                         Y + (int64_t)(row - row_begin) * ldy, F, f,
-                                         j < LR && f < F_load, vec_store != 0, lane, accum != 0);
+            if (heavy_pairs & 16)
+                row_pairs_pipe<kPairsU, O32, true>(col, val, k0, k1, X, ldx,
+                                                   Y + (int64_t)(row - row_begin) * ldy, F, f,
+                                                   j < LR && f < F_load, vec_store != 0, lane,
+                                                   accum != 0);
+            else
+                row_pairs_pipe<kPairsU, O32>(col, val, k0, k1, X, ldx,
+                                             Y + (int64_t)(row - row_begin) * ldy, F, f,
+                                             j < LR && f < F_load, vec_store != 0, lane, accum != 0);
             return;
         }
         const int sub = slice * n_sub + (wave - h * n_sub);  // in units of 64*VH floats
@@ -1264,10 +1426,14 @@ constexpr int kHeavyU = 16;
 // instead of one wave per 64*VH-float sub-chunk (row_chunks_pipe): bit 0 = in
 // the multi-row kernel (Reddit shape K=2: 9.29 -> 9.12 ms, profiles/r03/s1/ab.log),
 // bit 1 = in the one-row kernel; bit 2 = four nonzeros per load instead of two
-// in the multi-row kernel when a row has at most 16 lanes (launches of <= 64
-// floats, or 64-float slices: row_quads_pipe).
+// in the multi-row kernel on launches of <= 32 floats (row_quads_pipe); bit 3
+// = the same on 33..64-float launches, transposed (row_quadsT_pipe: one
+// 64-float hop over all Reddit-shape rows 0.715 -> 0.539 ms); bit 4 = the
+// pairs transposed (row_pairs_pipe TR: 76 floats 0.775 -> 0.747 ms, 304
+// floats 2.26 -> 2.16, Reddit K=2 8.11 -> 8.00; profiles/r04/quadsT_ab.log,
+// pairsT_ab.log; all bit-identical).
 // Set through sgc_set_tuning("heavy_pairs").
-static int g_heavy_pairs = 5;
+static int g_heavy_pairs = 29;
 // One-row kernel: row_chunks_pipe2 (whole-block schedule) on launches of at
 // least this many rows, row_chunks_pipe below.  Measured bit-identical,
 // interleaved (profiles/r03/s5/chunks_*.log): RMAT shape K=3 (4.2 M rows)
@@ -1325,6 +1491,8 @@ constexpr int64_t kWideRowsMin = 65536;
 template <int LB, int VH, bool O32, int QV>
 hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int R = kWave / LR, SW = LR * 4;
+    // each light row stages LB (col, val) pairs in its wave's 64-entry LDS block
+    if (LR <= 0 || R * LB > kWave) return hipErrorInvalidValue;
     const int slices = (F_load + SW - 1) / SW;
     // heavy sub-chunks per slice (unpacked heavy rows): whole 64*VH-float
     // chunks of a slice, or of the launch's width when it is a single slice
@@ -1340,7 +1508,7 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU, O32, QV>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
                        n_light_items, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
-                       a.heavy_threshold, a.accum, a.light_rows, g_heavy_pairs & 1);
+                       a.heavy_threshold, a.accum, a.light_rows, g_heavy_pairs & 17);
     return hipGetLastError();
 }
 
@@ -1418,7 +1586,7 @@ int set_tuning(const char *key, int64_t value) {
         return SGC_OK;
     }
     if (std::string(key) == "heavy_pairs") {
-        SGC_REQUIRE(value >= 0 && value <= 7, SGC_EINVAL, "heavy_pairs must be 0..7 (a bit mask)");
+        SGC_REQUIRE(value >= 0 && value <= 31, SGC_EINVAL, "heavy_pairs must be 0..31 (a bit mask)");
         g_heavy_pairs = (int)value;
         return SGC_OK;
     }
@@ -1615,8 +1783,12 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         // 0.667 -> 0.615 ms, but 48 and 64 floats slower (0.68 -> 0.82, 0.72
         // -> 0.85) and 64-float slices at full width far slower (3.8 -> 5.8):
         // there the pairs stay
-        const int qv = ((g_heavy_pairs & 4) && LR <= 16 && F4 <= 32) ? (F4 > 16 ? 2 : 1) : 0;
-        if (qv == 2)
+        int qv = ((g_heavy_pairs & 4) && LR <= 16 && F4 <= 32) ? (F4 > 16 ? 2 : 1) : 0;
+        // 33..64 floats: the transposed quads (row_quadsT_pipe, heavy_pairs bit 8)
+        if ((g_heavy_pairs & 8) && LR <= 16 && F4 > 32 && F4 <= 64) qv = 4;
+        if (qv == 4)  // the light rows' LDS block: LB * rows per wave <= 64
+            e = LR >= 16 ? SGC_ROWS(16, 2, 4) : SGC_ROWS(8, 2, 4);
+        else if (qv == 2)
             e = SGC_ROWS(8, 2, 2);
         else if (qv == 1)
             e = SGC_ROWS(8, 2, 1);

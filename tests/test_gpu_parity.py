@@ -320,24 +320,26 @@ def test_long_hub_rows_bit_exact(oracle, F, hub_chunk, hub_loaders):
         lib.sgc_set_tuning(b"hub_loaders", 15)
 
 
-@pytest.mark.parametrize("heavy_pairs", [1, 5])
+@pytest.mark.parametrize("heavy_pairs", [1, 5, 13, 17])
 @pytest.mark.parametrize("F", [1, 3, 4, 12, 16, 17, 30, 32, 33, 36, 44, 60, 64, 76, 96, 100, 124,
                                152])
 def test_narrow_launches_rows_kernel(oracle, F, heavy_pairs):
     """Feature widths below a slice (the feature partition's column blocks,
     the row partition's narrow groups): spmm_rows_kernel packs 64 // (F/4)
     rows into a wave.  Heavy rows (threshold 40) and hub rows (500) on the
-    same launch, heavy rows two nonzeros per load (heavy_pairs 1) or, up to
-    64 floats, four (5: row_quads_pipe with 4-, 2- or 1-float lanes); X in
+    same launch, heavy rows two nonzeros per load (heavy_pairs 1) or four:
+    up to 32 floats row_quads_pipe with 2- or 1-float lanes (5), at 33..64
+    floats the transposed quads (13: row_quadsT_pipe, 16-B lanes); X in
     128-B rows so hop 1 also takes 16-B lanes."""
     from sgc_amd import _lib, graphs
     from sgc_amd.propagate import DeviceCSR, propagate
     lib = _lib.load()
+    prev = lib.sgc_get_tuning(b"heavy_pairs")
     _lib.check(lib.sgc_set_tuning(b"heavy_pairs", heavy_pairs), "set_tuning")
     try:
         _narrow_case(oracle, F)
     finally:
-        lib.sgc_set_tuning(b"heavy_pairs", 5)
+        lib.sgc_set_tuning(b"heavy_pairs", prev)
 
 
 def _narrow_case(oracle, F):
@@ -550,7 +552,7 @@ def test_linear_tile_edges(tile_buffers, M, K, C, ld_extra):
             _, _, _, logits = linear_xent(Xd, W.to(DEV), b.to(DEV), y.to(DEV), want_logits=True)
             torch.testing.assert_close(logits.cpu().double(), ref, rtol=1e-5, atol=tol)
     finally:
-        lib.sgc_set_tuning(b"tile_buffers", 2)
+        lib.sgc_set_tuning(b"tile_buffers", 1)
 
 
 def test_sgc_model_autograd_matches_torch():
