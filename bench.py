@@ -430,6 +430,37 @@ def build_dist_step(args, S, X0, dev, rank, world, K, output, timing):
         par = (f"feature-partition x{world} ({fB}-column blocks, all K hops local) + {backend} "
                f"{exch}; output {output}")
         unit = f"rank 0's SpMM launches, {int(fb[1] - fb[0])} feature columns"
+    elif args.partition == "lines":
+        from sgc_amd.distributed import (LinePartitionedPropagator, _default_spmm, line_bounds,
+                                         make_shard)
+        from sgc_amd.propagate import spmm as spmm_hip
+        csr = DeviceCSR.from_host_arrays(S.row_ptr, S.col_idx, S.val, device=dev)
+        rp = np.asarray(S.row_ptr, dtype=np.int64)
+        shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
+
+        def main_bytes(X, r0, r1, out, flags=0):
+            nz, w = int(rp[r1] - rp[r0]), X.shape[1]
+            return 4 * (r1 - r0 + 1) + 8 * nz + 4 * w * n + 4 * w * (r1 - r0)
+
+        def tail_bytes(sh, X, out, *rest):
+            w = X.shape[1]
+            return 4 * (sh.rows + 1) + 8 * sh.nnz + 4 * w * n + 4 * w * sh.rows
+
+        prop = LinePartitionedPropagator(
+            shard, csr=csr,
+            main_spmm_fn=bracket(lambda X, r0, r1, out, flags=0: spmm_hip(
+                csr, X, r0, r1, out=out, flags=flags, threshold=args.threshold,
+                hub_threshold=args.hub_threshold), main_bytes),
+            tail_spmm_fn=bracket(_default_spmm, tail_bytes),
+            chunks=args.chunks, host_staging=staging)
+        prop._padded_ok = True  # the bracketed engine launches take the pad flags
+        W, T = line_bounds(F, world)
+        exch = ("one all-to-all of the main blocks' rows of X_K" if output == "sharded" else
+                f"one all-gather of X_K pipelined with the last hop in {args.chunks} row chunks")
+        par = (f"line-partition x{world} ({W}-column line blocks over all rows, all K hops "
+               f"local; the {F - T} tail columns by nnz-balanced row blocks, all-gathered after "
+               f"each hop on a tail stream) + {backend} {exch}; output {output}")
+        unit = f"rank 0's SpMM launches ({W}-column main block + its tail rows)"
     elif args.partition == "cyclic":
         from sgc_amd.distributed import CyclicRowPropagator, _cyclic_spmm
 
@@ -554,7 +585,7 @@ def main():
     ap.add_argument("--distributed-path", action="store_true",
                     help="run the N>1 path even at N=1 (exercises RCCL on one GPU)")
     ap.add_argument("--partition", default="auto",
-                    choices=["auto", "rows", "tiles", "cyclic", "features"],
+                    choices=["auto", "rows", "tiles", "cyclic", "features", "lines"],
                     help="N>1: split the rows of S (per-hop all-gather), rows x feature blocks "
                          "(tiles, --col-blocks), round-robin row tiles with column-ordered "
                          "exchange (cyclic), the feature columns (no exchange between hops, "
@@ -671,7 +702,7 @@ def main():
     torch.cuda.synchronize()
     warm_s = warmup(dev)  # what the drop-in loaders do on every rank
     _, first_pub = sgc_precompute(X0, adj, K)  # ingest + partition set-up + K hops
-    partition = multigpu.partition_name()
+    partition = multigpu.partition_name(world)
     launches = LaunchTimer(1)
 
     def public_step():
@@ -691,7 +722,7 @@ def main():
         tm = {"on": False, "pairs": [], "bytes": []}
         if args.partition == "auto":
             import copy
-            cands = ["rows", "cyclic", "features"]
+            cands = ["rows", "cyclic", "features", "lines"]
             if world >= 4 and world % args.col_blocks == 0:
                 cands.append("tiles")
             trials = {}
@@ -733,27 +764,42 @@ def main():
                     "loader_warmup_seconds": round(warm_s, 4),
                     "lib_sha256": lib_sha})
         if span:
-            # rank 0's SpMM launches; at the feature partition a launch is one
-            # hop over all rows at the rank's block width -- the compulsory
-            # bytes (S once, the block of X once, its Y once) are the basis,
-            # the same model as N = 1's `compulsory_frac`
-            w = int(fb[1] - fb[0]) if partition == "features" else None
-            t_l = float(np.mean(span)) * 1e-3
-            cb = (4 * (n + 1) + 8 * nnz + 8 * w * n) if w else None
+            # rank 0's SpMM launches over one step: the compulsory bytes of its
+            # K hops (S once, its block of X once, its Y once -- the same model
+            # as N = 1's `compulsory_frac`) over the launches' summed spans
+            # (launches on concurrent streams counted in full: conservative)
+            cb = None
+            if partition == "features":
+                w = int(fb[1] - fb[0])
+                cb = K * (4 * (n + 1) + 8 * nnz + 8 * w * n)
+                unit = f"rank 0's K hops over all {n} rows at its {w}-column block"
+            elif partition == "lines":
+                from sgc_amd.distributed import line_bounds, nnz_balanced_bounds
+                W, T = line_bounds(F, world)
+                wt = F - T
+                b = nnz_balanced_bounds(S.row_ptr, world)
+                rows0 = int(b[1] - b[0])
+                nnz0 = int(S.row_ptr[b[1]] - S.row_ptr[b[0]])
+                cb = K * ((4 * (n + 1) + 8 * nnz + 8 * min(W, F) * n if W else 0) +
+                          (4 * (rows0 + 1) + 8 * nnz0 + 4 * wt * (n + rows0) if wt else 0))
+                unit = (f"rank 0's K hops: all {n} rows at its {W}-column line block + its "
+                        f"{rows0} tail rows at the {wt} tail columns")
+            t_step = float(np.sum(span)) * 1e-3 / args.steps
             rec["roofline"] = {
                 "bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "kernel": (f"{kernel} (+ spmm_hub_kernel beside it, joined)" if hub else
                            str(kernel)),
-                "kernel_mean_ms": t_l * 1e3, "launches": len(span),
-                "launch_unit": (f"rank 0's hop over all {n} rows at its {w}-column block"
-                                if w else "rank 0's SpMM launches"),
-                "achieved": cb / t_l / 1e9 if cb else None,
-                "frac": cb / t_l / 1e9 / HBM_PEAK_GBS if cb else None,
-                "compulsory_bytes_per_launch": cb,
-                "compulsory_frac": cb / t_l / 1e9 / HBM_PEAK_GBS if cb else None,
+                "kernel_mean_ms": float(np.mean(span)), "launches": len(span),
+                "launch_unit": unit if cb else "rank 0's SpMM launches",
+                "launch_ms_per_step": t_step * 1e3,
+                "achieved": cb / t_step / 1e9 if cb else None,
+                "frac": cb / t_step / 1e9 / HBM_PEAK_GBS if cb else None,
+                "compulsory_bytes_per_step": cb,
+                "compulsory_frac": cb / t_step / 1e9 / HBM_PEAK_GBS if cb else None,
                 "traffic": None,
-                "achieved_basis": "compulsory bytes (S, the block of X and its Y once) per launch; "
-                                  "N = 1's roofline carries the same basis as compulsory_frac"}
+                "achieved_basis": "compulsory bytes (S, the block of X and its Y once) of rank "
+                                  "0's launches per step over their summed spans; N = 1's "
+                                  "roofline carries the same basis as compulsory_frac"}
         rec["precompute_seconds"] = rec["ms_per_step"] / 1e3
         if sharded is not None:
             rec["sharded_output"] = sharded

@@ -1,7 +1,8 @@
 """Bit-exactness of the N-rank paths at full BASELINE size, rehearsed on ONE GPU.
 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
-        scripts/dist_check.py [--shape reddit] [--partition rows|tiles] [--col-blocks 2]
+        scripts/dist_check.py [--shape reddit] [--partition rows|tiles|cyclic|features|lines]
+                              [--col-blocks 2]
 
 Every rank drives the same GPU (cuda:0) with the gloo backend (host-staged
 all-gathers, so no RCCL peer access is needed), runs the exact product
@@ -31,7 +32,7 @@ from sgc_amd.distributed import RowPartitionedPropagator, TiledPropagator, make_
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="reddit")
-    ap.add_argument("--partition", default="rows", choices=["rows", "tiles", "cyclic", "features"])
+    ap.add_argument("--partition", default="rows", choices=["rows", "tiles", "cyclic", "features", "lines"])
     ap.add_argument("--groups", type=int, default=4, help="cyclic: column groups")
     ap.add_argument("--tile", type=int, default=64, help="cyclic: rows per tile")
     ap.add_argument("--col-blocks", type=int, default=2)
@@ -40,6 +41,8 @@ def main():
     ap.add_argument("--exchange", default="auto", choices=["auto", "alltoall", "pairwise"],
                     help="features: the sharded exchange")
     ap.add_argument("--pieces", type=int, default=None, help="features: pairwise row pieces")
+    ap.add_argument("--also-replicated", action="store_true",
+                    help="lines: also check the replicated output against the sharded rows")
     ap.add_argument("--device", default="cuda", help="cpu: the CPU-twin rehearsal")
     ap.add_argument("--cache", default=os.environ.get("TMPDIR", "/tmp"))
     args = ap.parse_args()
@@ -89,6 +92,20 @@ def main():
         fp = FeaturePartitionedPropagator(csr, host_staging=True, exchange=args.exchange,
                                           pieces=args.pieces)
         mine = fp.propagate(X, K, output="sharded")
+        rb = equal_row_bounds(g["n"], world)
+        r0, r1 = int(rb[rank]), int(rb[rank + 1])
+    elif args.partition == "lines":
+        from sgc_amd.distributed import LinePartitionedPropagator, equal_row_bounds
+        from sgc_amd.propagate import DeviceCSR
+        csr = DeviceCSR.from_host_arrays(np.asarray(S.row_ptr), np.asarray(S.col_idx),
+                                         np.asarray(S.val), device=dev)
+        shard = make_shard(S.row_ptr, S.col_idx, S.val, rank, world, dev)
+        lp = LinePartitionedPropagator(shard, csr=csr, host_staging=True)
+        mine = lp.propagate(X, K, output="sharded")
+        if args.also_replicated:  # every rank's full X_K must equal the sharded rows
+            full = lp.propagate(X, K, output="replicated")
+            rb = equal_row_bounds(g["n"], world)
+            assert torch.equal(full[int(rb[rank]):int(rb[rank + 1])], mine)
         rb = equal_row_bounds(g["n"], world)
         r0, r1 = int(rb[rank]), int(rb[rank + 1])
     elif args.partition == "tiles":

@@ -1321,9 +1321,12 @@ struct LaunchArgs {
     int n_light;
 };
 
-// A side stream + fork/join events per (device, priority) for the hub kernel
-// (runs beside the main kernel; ordered against the caller's stream by
-// events, so the pair is capturable into a hipGraph).  The whole fork ->
+// A side stream + fork/join events per (device, caller's stream) for the
+// light kernel of a concurrent launch (the hub kernel stays on the caller's
+// stream; the two are ordered against it by events, so the pair is
+// capturable into a hipGraph).  One side stream per caller stream, so two
+// callers' launches on different streams (the line partition's main and tail
+// launches) never queue behind each other on a shared side stream.  The whole fork ->
 // launch -> join sequence of one sgc_spmm call runs under `mu`: another host
 // thread can neither re-record `fork` between this call's record and wait
 // (which would order the hub kernel after the wrong stream) nor enqueue on
@@ -1334,14 +1337,14 @@ struct SideStream {
     std::mutex mu;
 };
 
-hipError_t side_stream(SideStream **out) {
+hipError_t side_stream(SideStream **out, hipStream_t caller) {
     static std::mutex mu;
-    static std::map<int, SideStream> per_dev;
+    static std::map<std::pair<int, hipStream_t>, SideStream> per_dev;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> lock(mu);
-    SideStream &ss = per_dev[dev];
+    SideStream &ss = per_dev[{dev, caller}];
     if (!ss.s) {
         // (a highest-priority side stream measured neutral, +-1%:
         // profiles/r01_hub_priority_sweep.log)
@@ -1678,7 +1681,7 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         const bool serial =
             g_hub_stream == 2 || (g_hub_stream == 0 && (flags & SGC_SPMM_HUB_SERIAL));
         if (!hub_only && !serial) {
-            SGC_HIP_CHECK(side_stream(&side));
+            SGC_HIP_CHECK(side_stream(&side, stream));
             side_lock = std::unique_lock<std::mutex>(side->mu);
             SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
             SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));

@@ -1345,6 +1345,244 @@ class FeaturePartitionedPropagator:
 
 
 # ---------------------------------------------------------------------------
+# Line partition: whole 128-B lines of features per rank + a row-sharded tail.
+
+def line_bounds(F, world_size, line=32):
+    """Feature layout of the line partition: every rank owns W = m*line
+    columns (m = ceil(F/line) // P whole 128-B lines) -- main block p is
+    [min(p*W, F), min((p+1)*W, F)) -- and the tail [T, F), T = min(P*W, F),
+    is computed by row blocks.  Returns (W, T)."""
+    lines = -(-F // line)
+    W = (lines // world_size) * line
+    return W, min(F, world_size * W)
+
+
+class LinePartitionedPropagator:
+    """X_K = S^K X_0 with each rank owning whole 128-B lines of features plus
+    a row block of the leftover (tail) features.
+
+    What a hop costs on the GPU follows the 128-B lines each gathered row
+    segment touches: one GPU gathers ceil(F/32) lines per
+    nonzero (19 at F = 602); the feature partition's 76-float blocks gather 3
+    per nonzero on EVERY rank at P = 8 (24 in all), 152-float blocks 5 at
+    P = 4 (20).  Here rank p gathers m = ceil(F/32) // P whole lines over all
+    rows -- main block [p*W, (p+1)*W), W = 32m floats, no exchange between
+    hops, as in the feature partition -- and the tail's L - P*m lines (3 at F =
+    602 for P = 4 and 8) over its nnz-balanced row block only, so every rank
+    gathers m + (L - P*m)/P lines per nonzero: 2.375 at P = 8, 4.75 at P = 4.
+    The tail's row blocks are all-gathered after each hop into the [P*B, wt]
+    exchange buffer (B = the largest block) that the next hop's tail launch
+    reads through the shard's gathered column ids (RowPartitionedPropagator's
+    layout).  On the GPU the tail launches and their gathers run on a stream
+    of their own beside the main launches: a tail launch is small (1/P of
+    the nonzeros) and pays its ramp, its launch tail and its hub chains in
+    full when it runs alone, and the gather of hop k then rides under main
+    hop k as well.
+
+    Every element is still one FMA chain in CSR order: bit-identical to one
+    GPU and to the reference.
+
+    output="replicated": every rank gets X_K (the main blocks of the last hop
+    all-gathered in row chunks as they are computed, the tail from the last
+    gather); output="sharded": rank p gets rows [r_p, r_{p+1}) of X_K
+    (equal_row_bounds; the main blocks by one all-to-all).
+
+    main_spmm_fn(X, r0, r1, out, flags=0) computes rows [r0, r1) of S.X over
+    the full CSR (default: the HIP engine over `csr`); tail_spmm_fn(shard, X,
+    out, layout) computes the shard's rows (default: _default_spmm).  Tests
+    inject the CPU oracle for both."""
+
+    def __init__(self, shard: ShardCSR, csr=None, group=None,
+                 main_spmm_fn: Optional[Callable] = None,
+                 tail_spmm_fn: Optional[Callable] = None, chunks: int = 4,
+                 host_staging: bool = False):
+        self.shard = shard
+        self.group = group
+        self.rank, self.world_size = shard.rank, shard.world_size
+        self._padded_ok = main_spmm_fn is None
+        if main_spmm_fn is None:
+            if csr is None:
+                raise ValueError("LinePartitionedPropagator needs a DeviceCSR or a main_spmm_fn")
+            from .propagate import spmm
+
+            def main_spmm_fn(X, r0, r1, out, flags=0, _csr=csr):
+                return spmm(_csr, X, r0, r1, out=out, flags=flags)
+        self.main_spmm_fn = main_spmm_fn
+        self.tail_spmm_fn = tail_spmm_fn or _default_spmm
+        self.chunks = max(1, int(chunks))
+        self.host_staging = host_staging
+        self._bufs = {}
+        self._tail_stream = None
+
+    def _buf(self, key, shape, like):
+        b = self._bufs.get(key)
+        if b is None or tuple(b.shape) != tuple(shape) or b.device != like.device:
+            b = torch.empty(shape, dtype=torch.float32, device=like.device)
+            self._bufs[key] = b
+        return b
+
+    def _tail_ctx(self, device):
+        """Context running the tail's launches and gathers on the tail stream
+        (a no-op on the CPU)."""
+        import contextlib
+        if device.type != "cuda":
+            return contextlib.nullcontext()
+        if self._tail_stream is None or self._tail_stream.device != device:
+            self._tail_stream = torch.cuda.Stream(device)
+        return torch.cuda.stream(self._tail_stream)
+
+    def _collective(self, kind, dst, src):
+        if self.world_size == 1:
+            return _local_copy(dst, src)
+        fn = dist.all_gather_into_tensor if kind == "gather" else dist.all_to_all_single
+        if not self.host_staging:
+            return fn(dst, src, group=self.group, async_op=True)
+        h = torch.empty(dst.shape, dtype=dst.dtype)
+        fn(h, src.cpu(), group=self.group)
+        dst.copy_(h)
+        return None
+
+    def _tail_rows(self, full, wt, r0, r1, dst):
+        """dst[:] = tail rows [r0, r1) of the gathered [P*B, ld] buffer (they
+        may span several ranks' blocks)."""
+        sh = self.shard
+        B = sh.block
+        for q in range(self.world_size):
+            a, b = max(r0, int(sh.bounds[q])), min(r1, int(sh.bounds[q + 1]))
+            if b > a:
+                s = q * B + a - int(sh.bounds[q])
+                _copy_cols(full[s:s + b - a, :wt], dst[a - r0:b - r0])
+
+    def propagate(self, X0, K, out=None, output="replicated"):
+        if output not in ("replicated", "sharded"):
+            raise ValueError(f"output must be 'replicated' or 'sharded', not {output!r}")
+        n, F = X0.shape
+        P, p = self.world_size, self.rank
+        sh = self.shard
+        if sh.n != n:
+            raise ValueError(f"shard has {sh.n} nodes, features {n}")
+        rb = equal_row_bounds(n, P)
+        if K <= 0:
+            return X0 if output == "replicated" else X0[int(rb[p]):int(rb[p + 1])]
+        W, T = line_bounds(F, P)
+        c0, c1 = min(p * W, F), min((p + 1) * W, F)
+        w, wt = c1 - c0, F - T
+        gpu = X0.is_cuda
+        ld = (max(W, 1) + 31) // 32 * 32 if gpu else max(W, 1)
+        ldt = (max(wt, 1) + 31) // 32 * 32 if gpu else max(wt, 1)
+        if out is None:
+            shape = (n, F) if output == "replicated" else (int(rb[p + 1] - rb[p]), F)
+            out = torch.empty(shape, dtype=torch.float32, device=X0.device)
+        from .propagate import SPMM_X_PADDED, SPMM_Y_PADDED
+
+        def main_hop(src, r0, r1, dst, own_src, own_dst):
+            if self._padded_ok:
+                fl = (SPMM_X_PADDED if own_src else 0) | (SPMM_Y_PADDED if own_dst else 0)
+                return self.main_spmm_fn(src, r0, r1, dst, flags=fl)
+            return self.main_spmm_fn(src, r0, r1, dst)
+
+        def aligned(v, col0, width):  # 16-B lanes readable in place
+            return (not gpu or (width % 4 == 0 and col0 % 4 == 0 and v.stride(0) % 4 == 0 and
+                                v.data_ptr() % 16 == 0))
+
+        # hop-1 inputs: the rank's main block and the tail, in 128-B rows
+        msrc, mown = X0[:, c0:c1], False
+        if w and K > 1 and not aligned(X0, c0, w):
+            a = self._buf("a", (n, ld), X0)
+            _copy_cols(X0[:, c0:c1], a[:, :w])
+            msrc, mown = a[:, :w], True
+        # tail launches on the engine's own 128-B-row buffers compute wt
+        # rounded up to 4 columns (16-B lanes; the pad columns are never read
+        # back), on the caller's X_0 exactly wt
+        wt4 = min(ldt, (wt + 3) // 4 * 4) if gpu else wt
+        tsrc, tlayout, tw = X0[:, T:F], "input", wt
+        if wt and gpu and not aligned(X0, T, wt):
+            ta = self._buf("ta", (n, ldt), X0)
+            _copy_cols(X0[:, T:F], ta[:, :wt])
+            tsrc, tw = ta[:, :wt4], wt4
+        B = sh.block
+        work = None
+        full = None
+        if gpu and wt:  # the tail stream starts after the inputs (and last call)
+            cur = torch.cuda.current_stream(X0.device)
+            with self._tail_ctx(X0.device):
+                torch.cuda.current_stream(X0.device).wait_stream(cur)
+        for k in range(1, K + 1):
+            # tail: this rank's rows of hop k, gathered at once for hop k+1
+            if wt:
+                with self._tail_ctx(X0.device):
+                    if work is not None:
+                        work.wait()
+                    loc = self._buf(("tl", k & 1), (B, ldt), X0)
+                    if sh.rows:
+                        self.tail_spmm_fn(sh, tsrc, loc[:sh.rows, :tw], tlayout)
+                    full = self._buf(("tf", k & 1), (P * B, ldt), X0)
+                    work = self._collective("gather", full, loc)
+                    if work is None and gpu:  # staged: the copy is done on this stream
+                        work = _StreamDone(torch.cuda.current_stream(X0.device))
+                tsrc, tlayout, tw = full[:, :wt4], "gathered", wt4
+            # main block of hop k (no exchange between hops)
+            if k < K:
+                dst = self._buf(("h", k & 1), (n, ld), X0)[:, :w]
+                if w and n:
+                    main_hop(msrc, 0, n, dst, mown, True)
+                msrc, mown = dst, True
+                continue
+            if output == "replicated":
+                self._last_replicated(msrc, mown, out, main_hop, W, w, ld, P, X0)
+            else:
+                self._last_sharded(msrc, mown, out, main_hop, W, w, rb, P, X0)
+        if work is not None:
+            work.wait()
+        if wt:  # the tail of X_K from the last gather
+            r0, r1 = (0, n) if output == "replicated" else (int(rb[p]), int(rb[p + 1]))
+            self._tail_rows(full, wt, r0, r1, out[:, T:F])
+        return out
+
+    def _last_replicated(self, msrc, mown, out, main_hop, W, w, ld, P, X0):
+        n, F = out.shape
+        if P == 1:
+            if w and n:
+                main_hop(msrc, 0, n, out[:, :w], mown, False)
+            return
+        pending = []
+        for ci, (r0, r1) in enumerate(row_chunks(n, self.chunks)):
+            rows = r1 - r0
+            loc = self._buf(("loc", ci), (rows, ld), X0)
+            if w and rows:
+                main_hop(msrc, r0, r1, loc[:, :w], mown, True)
+            full = self._buf(("full", ci), (P * rows, ld), X0)
+            pending.append((r0, r1, full, self._collective("gather", full, loc) if rows else None))
+        for r0, r1, full, work in pending:
+            if work is not None:
+                work.wait()
+            rows = r1 - r0
+            for q in range(P):
+                q0, q1 = min(q * W, F), min((q + 1) * W, F)
+                if q1 > q0 and rows:
+                    _copy_cols(full[q * rows:(q + 1) * rows, :q1 - q0], out[r0:r1, q0:q1])
+
+    def _last_sharded(self, msrc, mown, out, main_hop, W, w, rb, P, X0):
+        n = msrc.shape[0]
+        F = out.shape[1]
+        p = self.rank
+        Bn = max(1, -(-n // P))
+        ldw = max(W, 1)
+        send = self._buf("send", (P * Bn, ldw), X0)
+        if w and n:
+            main_hop(msrc, 0, n, send[:n, :w], mown, True)
+        recv = self._buf("recv", (P * Bn, ldw), X0)
+        work = self._collective("a2a", recv, send)
+        if work is not None:
+            work.wait()
+        rows = int(rb[p + 1] - rb[p])
+        for q in range(P):
+            q0, q1 = min(q * W, F), min((q + 1) * W, F)
+            if q1 > q0 and rows:
+                _copy_cols(recv[q * Bn:q * Bn + rows, :q1 - q0], out[:, q0:q1])
+
+
+# ---------------------------------------------------------------------------
 # Data-parallel classifier over a row-sharded X_K.
 
 def _torch_loss_grad(X, W, b, y):

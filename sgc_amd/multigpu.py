@@ -17,11 +17,16 @@ either of two ways:
   native multi-device engine of the C ABI (sgc_mgpu_*, csrc/mgpu.hip) drives
   all of them from the single call; see `DeviceSet`.
 
-Partition (SGC_AMD_PARTITION): "features" (default) -- each rank runs all K
-hops over the whole S on its block of feature columns, so the only exchange
-is one all-gather of X_K, the least any replicated output can move; "rows"
-(nnz-balanced row blocks, an all-gather of X_k per hop: the north star's 1-D
-row slicing) or "cyclic" (row tiles round-robin, column-ordered exchange).
+Partition (SGC_AMD_PARTITION): "auto" (default) = "lines" from 4 ranks,
+"features" below; "features" -- each rank runs all K hops over the whole S on
+its block of feature columns, so the only exchange is one all-gather of X_K,
+the least any replicated output can move; "lines" -- each rank owns whole
+128-B lines of features plus a row block of the leftover lines, gathered
+after each hop (per-rank compute at Reddit shape, one GPU per rank: P = 4
+2.44 vs 3.03 ms, P = 8 1.52 vs 1.62; P = 2 5.44 vs 5.19, DESIGN.md 6.3);
+"rows" (nnz-balanced row blocks, an all-gather of X_k per hop: the north
+star's 1-D row slicing) or "cyclic" (row tiles round-robin, column-ordered
+exchange).
 Every partition keeps each output element's FMA chain whole and in CSR
 order, so X_K is bit-identical to one GPU's and to the reference.
 """
@@ -30,7 +35,7 @@ import os
 import torch
 import torch.distributed as dist
 
-PARTITIONS = ("features", "rows", "cyclic")
+PARTITIONS = ("auto", "features", "lines", "rows", "cyclic")
 
 
 def torchrun_env():
@@ -91,10 +96,15 @@ def process_group(device):
     return dist.group.WORLD
 
 
-def partition_name():
-    p = os.environ.get("SGC_AMD_PARTITION", "features")
+def partition_name(world=None):
+    """The partition SGC_AMD_PARTITION names; "auto" (the default) resolves
+    to "lines" at world >= 4 and "features" below (returned as "auto" when
+    no world size is given)."""
+    p = os.environ.get("SGC_AMD_PARTITION", "auto")
     if p not in PARTITIONS:
         raise ValueError(f"SGC_AMD_PARTITION must be one of {PARTITIONS}, not {p!r}")
+    if p == "auto" and world is not None:
+        return "lines" if world >= 4 else "features"
     return p
 
 
@@ -111,7 +121,7 @@ def _propagator(csr, group, partition, staging):
     """The partitioned propagator for (adjacency, group, partition), built once
     and cached on the adjacency's CSR with its buffers and prepared launches."""
     from .distributed import (CyclicRowPropagator, FeaturePartitionedPropagator,
-                              RowPartitionedPropagator, make_shard)
+                              LinePartitionedPropagator, RowPartitionedPropagator, make_shard)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     key = ("dist", id(group), rank, world, partition, staging)
     prop = csr._plans.get(key)
@@ -120,6 +130,10 @@ def _propagator(csr, group, partition, staging):
     if partition == "features":
         prop = FeaturePartitionedPropagator(csr, rank=rank, world_size=world, group=group,
                                             host_staging=staging)
+    elif partition == "lines":
+        rp, ci, va = _host_csr(csr)
+        shard = make_shard(rp, ci, va, rank, world, csr.device)
+        prop = LinePartitionedPropagator(shard, csr=csr, group=group, host_staging=staging)
     elif partition == "rows":
         rp, ci, va = _host_csr(csr)
         shard = make_shard(rp, ci, va, rank, world, csr.device)
@@ -138,7 +152,7 @@ def precompute_group(csr, X, K, group):
     checked shapes and devices).  Collective: every rank must call it with
     the same adjacency and feature shape."""
     staging = X.is_cuda and dist.get_backend(group) != "nccl"
-    prop = _propagator(csr, group, partition_name(), staging)
+    prop = _propagator(csr, group, partition_name(dist.get_world_size(group)), staging)
     return prop.propagate(X, K, output="replicated")
 
 

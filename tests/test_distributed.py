@@ -15,9 +15,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from sgc_amd.distributed import (FeaturePartitionedPropagator, RowPartitionedPropagator,
-                                 equal_row_bounds, feature_bounds, make_shard,
-                                 nnz_balanced_bounds, row_chunks)
+from sgc_amd.distributed import (FeaturePartitionedPropagator, LinePartitionedPropagator,
+                                 RowPartitionedPropagator, equal_row_bounds, feature_bounds,
+                                 line_bounds, make_shard, nnz_balanced_bounds, row_chunks)
 
 
 def _free_port():
@@ -384,6 +384,73 @@ def test_feature_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, ch
     procs = [ctx.Process(target=_feature_worker,
                          args=(r, world, port, case, K, q, chunks, align, staging, output,
                                exchange, pieces))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _check_results(results, case, K, world, output, name)
+
+
+# ---------------------------------------------------------------------------
+# Line partition: whole 128-B lines per rank + a row-sharded tail.
+
+def test_line_bounds():
+    assert line_bounds(602, 8) == (64, 512)    # 19 lines: 2 per rank + 3 tail lines
+    assert line_bounds(602, 4) == (128, 512)   # 4 per rank + 3
+    assert line_bounds(602, 2) == (288, 576)   # 9 per rank + 1 (26 floats)
+    assert line_bounds(602, 19) == (32, 602)   # every line its rank's, the last short
+    assert line_bounds(65, 4) == (0, 0)        # fewer lines than ranks: all tail
+    assert line_bounds(64, 2) == (32, 64)      # no tail
+    assert line_bounds(7, 1) == (32, 7)
+
+
+def _line_worker(rank, world, port, case, K, result_q, chunks, staging, output, balance):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as o
+        n = int(case["n"])
+        rp, ci, va = o.coo_to_csr(n, n, case["rows"], case["cols"], case["vals"])
+
+        def main_fn(X, r0, r1, out):
+            out.copy_(torch.from_numpy(o.spmm_csr(rp, ci, va, X.numpy(), r0, r1)))
+
+        shard = make_shard(rp, ci, va, rank, world, "cpu", balance=balance)
+        prop = LinePartitionedPropagator(shard, main_spmm_fn=main_fn, tail_spmm_fn=_oracle_spmm,
+                                         chunks=chunks, host_staging=staging)
+        X0 = torch.from_numpy(case["X"])
+        out = prop.propagate(X0, K, output=output)
+        out2 = prop.propagate(X0, K, output=output)  # buffers reused
+        assert torch.equal(out, out2)
+        result_q.put((rank, (out.numpy(), equal_row_bounds(n, world))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,name,K,chunks,staging,output,balance", [
+    (2, "norm_n48_F602", 2, 4, False, "replicated", "nnz"),   # 9 lines each + a 26-float tail
+    (2, "norm_n48_F602", 3, 2, False, "sharded", "nnz"),
+    (4, "norm_n48_F602", 2, 3, False, "replicated", "rows"),  # 4 lines each + 90-float tail
+    (3, "hub1000_F130", 2, 2, False, "sharded", "nnz"),       # 1 line each + 34-float tail
+    (4, "hub1000_F130", 2, 4, True, "replicated", "nnz"),     # 1 line each + 2-float tail
+    (3, "norm_n48_F65", 2, 3, False, "replicated", "nnz"),    # a line each (the last 1 float), no tail
+    (4, "raw_unsorted_dups_F7", 3, 5, False, "sharded", "nnz"),  # all tail
+    (2, "isolated_F17", 1, 1, True, "replicated", "nnz"),
+    (2, "norm_n48_F3", 2, 4, False, "sharded", "rows")])
+def test_line_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, chunks, staging,
+                                       output, balance):
+    """Main line blocks need no exchange; the tail's row blocks are gathered
+    after every hop and read through the gathered column ids (uneven nnz
+    blocks, so the gathered layout is not the identity)."""
+    case = tiny_cases[name]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_line_worker,
+                         args=(r, world, port, case, K, q, chunks, staging, output, balance))
              for r in range(world)]
     for p in procs:
         p.start()

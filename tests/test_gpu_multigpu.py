@@ -164,7 +164,7 @@ def test_mgpu_handles_survive_reinit(tiny_cases, oracle):
 # ---------------------------------------------------------------------------
 # sgc_precompute under torchrun, the reddit driver, bench.py self-launch
 
-@pytest.mark.parametrize("partition", ["features", "rows", "cyclic"])
+@pytest.mark.parametrize("partition", ["features", "lines", "rows", "cyclic"])
 def test_sgc_precompute_under_torchrun_matches_one_gpu(tmp_path, partition):
     """Two torchrun ranks sharing the GPU (gloo, chosen by the drop-in because
     there are fewer GPUs than ranks) run the unchanged sgc_precompute on the
@@ -230,6 +230,7 @@ def dist_cache(tmp_path_factory):
     ("reddit", "rows", ["--row-chunks", "4"]),
     ("reddit", "cyclic", ["--groups", "3"]),
     ("reddit", "features", []),
+    ("reddit", "lines", ["--also-replicated"]),
     ("reddit", "tiles", ["--col-blocks", "2"]),
     ("rmat", "rows", [])])
 def test_p8_partition_full_size_bit_exact(dist_cache, shape, partition, extra):

@@ -50,7 +50,8 @@ def _torchrun_like_worker(rank, world, port, case, K, partition, q):
     (3, "raw_unsorted_dups_F7", 3, "features"), (2, "special_values_F11", 2, "rows"),
     (2, "norm_n48_F65", 2, "rows"), (3, "norm_n48_F130", 2, "rows"),
     (2, "hub1000_F130", 2, "cyclic"), (4, "norm_n48_F65", 3, "cyclic"),
-    (2, "isolated_F17", 1, "features")])
+    (2, "isolated_F17", 1, "features"), (2, "norm_n48_F602", 2, "lines"),
+    (3, "hub1000_F130", 2, "lines"), (4, "norm_n48_F602", 2, "auto")])
 def test_sgc_precompute_under_torchrun_env(tiny_cases, world, name, K, partition):
     case = tiny_cases[name]
     ctx = mp.get_context("spawn")
@@ -105,4 +106,8 @@ def test_partition_name_checked(monkeypatch):
     with pytest.raises(ValueError, match="SGC_AMD_PARTITION"):
         multigpu.partition_name()
     monkeypatch.delenv("SGC_AMD_PARTITION")
-    assert multigpu.partition_name() == "features"
+    assert multigpu.partition_name() == "auto"
+    assert [multigpu.partition_name(w) for w in (2, 3, 4, 8)] == ["features", "features",
+                                                                   "lines", "lines"]
+    monkeypatch.setenv("SGC_AMD_PARTITION", "rows")
+    assert multigpu.partition_name(8) == "rows"
