@@ -207,7 +207,9 @@ int sgc_timing_collect(float *light_ms_host, float *hub_ms_host, int64_t capacit
 /* Same, plus per launch: span_ms_host[i] = the whole launch (first kernel
  * start to the later kernel end: what the caller's stream waits for) and
  * light_kernel_host[i] = which light/heavy-row kernel ran (0 spmm_csr_kernel,
- * 1 spmm_rows_kernel, -1 none: a hub-only launch).  Either may be NULL. */
+ * 1 spmm_rows_kernel, 2 / 3 spmm_rows_kernel / spmm_csr_kernel with the
+ * serial hub rows fused into its launch, -1 none: a hub-only launch).  Either
+ * may be NULL. */
 int sgc_timing_collect_ex(float *light_ms_host, float *hub_ms_host, float *span_ms_host,
                           int32_t *light_kernel_host, int64_t capacity, int64_t *n_host);
 

@@ -60,6 +60,8 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 // LDS image depth of the classifier tile (gemm_tile.h; linear.hip defines it,
 // sgc_set_tuning("tile_buffers") sets it: 1 or 2).
 extern int g_tile_buffers;
+// Classifier forward kernel (linear.hip): 0 auto, 1 LDS tile, 2 streaming.
+extern int g_linear_kernel;
 
 template <int V> struct Vec { typedef float __attribute__((ext_vector_type(V))) T; };
 template <> struct Vec<1> { typedef float T; };

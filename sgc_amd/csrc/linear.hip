@@ -42,6 +42,211 @@ __global__ __launch_bounds__(256) void linear_kernel(const float *__restrict__ X
     }
 }
 
+// ---------------------------------------------------------------------------
+// Streaming form (the default where W fits LDS): W^T lives in LDS for the
+// whole launch and every wave streams its own 16-row tiles of X straight from
+// HBM into MFMA operand registers -- no X staging through LDS, no barrier
+// after the one W load, so no wave ever waits for another.
+//
+// * Grid: one 1024-thread workgroup per CU (W's image is ~123 KB at 48 x 640),
+//   persistent; tile t (rows 16t..16t+15) goes to workgroup t mod grid, whose
+//   waves take their next tile from an LDS counter.
+// * Per 32-k chunk lane (i, g) loads row i's k0+4g .. +3 and k0+16+4g .. +3
+//   (two b128, or four b64 on 8-B aligned rows -- ldx = 602 is), so one load
+//   instruction reads 64 contiguous bytes of each of its 16 rows and each
+//   row's 128-B line is read once per chunk; the loads run kStreamDepth chunks ahead in a register ring
+//   (the wave's chunk stream runs on across tile boundaries, with running
+//   (tile, chunk) counters: no divisions), so each SIMD keeps ~4 x 4 x 2 KB of
+//   X in flight; a slot is reloaded after the MFMAs that read it (no copies).
+// * MFMA step kk of a chunk sums k = k0 + 16(kk >> 2) + 4g + (kk & 3) over g
+//   (any k permutation shared by both operands sums the same products; fp32
+//   MFMA products are exact), W's operands by ds_read_b128 from an
+//   XOR-swizzled image (conflict-free in every b128 lane group).
+// Measured before these last three points (profiles/r04/cls_diag*.log): the
+// same 0.128 ms as the LDS tile, with the loads alone 0.111 and the MFMAs
+// alone 0.108 -- per-chunk divisions, operand copies and 75 % LDS
+// bank-conflict cycles, not HBM or the MFMA pipe, set both.
+// * Loads go through one buffer descriptor over all of X: rows past M read
+//   zeros; the last chunk's k >= K are zeroed in registers (X beyond a row is
+//   the next row, and 0 x inf would be NaN).
+// MFMA work at 152,410 x 602 x 48 is 56 us at the fp32 peak and the X read
+// ~58 us at 6.3 TB/s: both pipes must run together.
+constexpr int kStreamDepth = 4;  // chunks in flight per wave
+constexpr int kStreamWaves = 16;
+
+// DIAG (diagnostics only, sgc_set_tuning("linear_kernel", 3 / 4)): 1 = the
+// loads and stores without the MFMAs (the X stream's own time), 2 = the MFMAs
+// on registers without the X loads (the MFMA pipe's own time).
+template <int V, int NT, int DIAG = 0>
+__global__ __launch_bounds__(64 * kStreamWaves) void linear_stream_kernel(
+    const float *__restrict__ X, int64_t ldx, const float *__restrict__ W,
+    const float *__restrict__ b, float *__restrict__ Y, int64_t ldy, int M, int K, int C,
+    int Kp) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    using VT = typename Vec<V>::T;
+    constexpr int NV = 8 / V;  // vector loads per lane per chunk
+    // W^T image [NT*16][S], S = K rounded up to 64 floats; the 16-B granule q
+    // of row r sits at granule q ^ (r & 15) of its 64-float window, so every
+    // ds_read_b128 lane group (4 x 16 lanes, MI355X_MICROARCH.md LDS table)
+    // hits 16 distinct 4-bank groups: lane (i, g) reads granule 8c + 4h + g
+    // of row n*16 + i (a plain stride leaves 2-way conflicts in two groups).
+    extern __shared__ __attribute__((aligned(16))) float sw[];
+    const int S = (K + 63) / 64 * 64;
+    // the wave index as a scalar: every tile / chunk counter below derives from
+    // it and stays in SGPRs, so the per-chunk control flow is scalar branches
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int i = lane & 15, g = lane >> 4;
+    // (eight independent loads in flight per thread: the image is ~30 loads
+    // per thread, which one at a time cost several microseconds of latency)
+    constexpr int kWU = 8;
+    for (int base = threadIdx.x; base < NT * 16 * S; base += kWU * 64 * kStreamWaves) {
+        float v[kWU];
+#pragma unroll
+        for (int u = 0; u < kWU; ++u) {
+            const int idx = base + u * 64 * kStreamWaves;
+            const int r = idx / S, k = idx - r * S;
+            v[u] = (idx < NT * 16 * S && r < C && k < K) ? W[(int64_t)r * K + k] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kWU; ++u) {
+            const int idx = base + u * 64 * kStreamWaves;
+            const int r = idx / S, k = idx - r * S;
+            if (idx < NT * 16 * S) sw[r * S + (((k >> 2) ^ (r & 15)) << 2) + (k & 3)] = v[u];
+        }
+    }
+    __syncthreads();
+    const int n_tiles = (M + 15) >> 4;
+    // Tiles are dealt per workgroup (t = block + grid * m, 37-38 per CU at the
+    // Reddit-train shape) and its 16 waves take the next m from an LDS counter
+    // as they go, so every wave stays busy until the CU's list is done (a fixed
+    // deal gave some waves 3 tiles and their SIMD-mates 2: the last third of
+    // the launch ran on a quarter of the waves).
+    int *next = reinterpret_cast<int *>(sw + NT * 16 * S);
+    if (threadIdx.x == 0) *next = 0;
+    __syncthreads();
+    (void)w;
+    auto grab = [&]() -> int {
+        int m = 0;
+        if (lane == 0) m = atomicAdd(next, 1);
+        m = __builtin_amdgcn_readfirstlane(m);
+        const int t = (int)blockIdx.x + (int)gridDim.x * m;
+        return t < n_tiles ? t : -1;
+    };
+    const int NC = Kp / 32;  // chunks per tile
+    const auto xd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(X), 0, (int)((int64_t)M * ldx * 4), 0x00020000);  // < 2^31
+    // loader: chunk lc of tile ltile (-1: the CU's list is done)
+    int ltile = grab(), lc = 0;
+    auto row_off = [&](int tile) -> uint32_t {
+        const int row = tile * 16 + i;
+        return (tile >= 0 && row < M) ? (uint32_t)((int64_t)row * ldx * 4) + 16u * g : kOffOOB;
+    };
+    uint32_t lrow = row_off(ltile);
+    VT xr[kStreamDepth][NV];
+    int stile[kStreamDepth], sc[kStreamDepth];  // each slot's (tile, chunk); tile -1 = none
+    auto load = [&](int slot_) {
+        stile[slot_] = ltile;
+        sc[slot_] = lc;
+        if (ltile < 0) return;
+        const uint32_t off = lrow + (uint32_t)lc * 128u;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            if constexpr (DIAG == 2)
+                xr[slot_][q] = VT{} + (float)(off & 7);
+            else  // element e = qV.. of the lane: byte 16g + 4(e & 3) + 64(e >> 2)
+                xr[slot_][q] = buffer_load_vec<V>(xd, off + ((q * V * 4) & 15) +
+                                                          ((q * V * 4) >> 4) * 64);
+        }
+        if (++lc == NC) {
+            lc = 0;
+            ltile = grab();
+            lrow = row_off(ltile);
+        }
+    };
+#pragma unroll
+    for (int u = 0; u < kStreamDepth; ++u) load(u);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // W operands of chunk c (granules 8c + 4h + g of rows n*16 + i, swizzled),
+    // read one chunk ahead into the other register set, so the MFMAs never
+    // wait for their LDS reads
+    f4 bw[2][NT][2];
+    auto read_w = [&](int c, f4 (&dst)[NT][2]) {
+        const int wbase = (c >> 1) * 64;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int col = wbase + (((((c & 1) << 3) + 4 * h + g) ^ i) << 2);
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                dst[n][h] = *reinterpret_cast<const f4 *>(&sw[(n * 16 + i) * S + col]);
+        }
+    };
+    // (at NT = 4 the second set would spill at the 128-VGPR cap of 16 waves:
+    // read in place there)
+    constexpr bool kPreW = NT <= 3;
+    if constexpr (kPreW) read_w(sc[0], bw[0]);
+    static_assert(kStreamDepth % 2 == 0, "the W register sets alternate per slot");
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < kStreamDepth; ++u) {
+            const int tile = stile[u], c = sc[u];
+            if (tile < 0) return;  // wave-uniform: the stream is in order, so all later slots are empty too
+            const int cur = kPreW ? (u & 1) : 0;  // a constant after unrolling
+            const int un = (u + 1) % kStreamDepth;
+            if constexpr (kPreW) {
+                if (stile[un] >= 0) read_w(sc[un], bw[cur ^ 1]);
+            } else {
+                read_w(c, bw[0]);
+            }
+            float a[8];
+#pragma unroll
+            for (int q = 0; q < NV; ++q)
+#pragma unroll
+                for (int e = 0; e < V; ++e) a[q * V + e] = lane_elem<V>(xr[u][q], e);
+            if ((c + 1) * 32 > K) {  // the ragged last chunk (uniform)
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (c * 32 + 16 * (e >> 2) + 4 * g + (e & 3) >= K) a[e] = 0.0f;
+            }
+            if constexpr (DIAG == 1) {
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk)
+                    acc[kk % NT][kk & 3] += a[kk] * bw[cur][0][0][kk & 3];
+            } else {
+#pragma unroll
+                for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+                    for (int n = 0; n < NT; ++n)
+                        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            a[kk], bw[cur][n][kk >> 2][kk & 3], acc[n], 0, 0, 0);
+            }
+            // the chunk kStreamDepth ahead into the slot just consumed
+            load(u);
+            if (c == NC - 1) {  // tile done: D[4g + r][i] = row 4g + r, class n*16 + i
+                const int m0 = tile * 16 + 4 * g;
+#pragma unroll
+                for (int n = 0; n < NT; ++n) {
+                    const int cl = n * 16 + i;
+                    if (cl >= C) continue;
+                    const float bias = b ? b[cl] : 0.0f;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (m0 + r < M) Y[(int64_t)(m0 + r) * ldy + cl] = acc[n][r] + bias;
+                }
+#pragma unroll
+                for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    }
+}
+
+
+// 0 = auto (streaming where W fits LDS and the rows are 8-B aligned), 1 = the
+// LDS tile, 2 = streaming (3 / 4: its DIAG forms, wrong results by design).
+// Set through sgc_set_tuning("linear_kernel").
+int g_linear_kernel = 0;
+
 // One LDS image per block (two barriers per chunk, half the LDS: twice the
 // blocks per CU) measured faster than the double buffer at the Reddit-train
 // shape: forward 0.128-0.130 vs 0.146-0.152 ms (profiles/r04/classifier_v3_*.log).
@@ -76,6 +281,40 @@ hipError_t dispatch_nt(int nt, const float *X, int64_t ldx, const float *W, cons
 
 }  // namespace
 
+template <int V, int NT, int DIAG = 0>
+hipError_t launch_stream(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
+                         int64_t ldy, int M, int K, int C, int Kp, size_t lds, hipStream_t s) {
+    static int cus = 0;
+    static bool attr[5] = {false, false, false, false, false};
+    if (!cus) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+    }
+    if (!attr[NT]) {
+        hipError_t e = hipFuncSetAttribute(
+            reinterpret_cast<const void *>(&linear_stream_kernel<V, NT, DIAG>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        attr[NT] = true;
+    }
+    // one workgroup per CU, at most one per tile
+    const int tiles = (M + 15) / 16;
+    const int blocks = std::max(1, std::min(cus, tiles));
+    hipLaunchKernelGGL((linear_stream_kernel<V, NT, DIAG>), dim3((unsigned)blocks),
+                       dim3(64 * kStreamWaves), lds, s, X, ldx, W, b, Y, ldy, M, K, C, Kp);
+    return hipGetLastError();
+}
+
+// Streaming kernel preconditions: W's image within LDS, X within 31-bit byte
+// offsets, rows 8-B aligned.
+bool stream_fits(int64_t M, int64_t K, int64_t ldx, int nt, const float *X, size_t *lds) {
+    *lds = (size_t)nt * 16 * ((K + 63) / 64 * 64) * 4 + 16;  // + the tile counter
+    return *lds <= 160 * 1024 && M * ldx * 4 < INT32_MAX && ldx % 2 == 0 &&
+           reinterpret_cast<uintptr_t>(X) % 8 == 0;
+}
+
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                       int64_t ldy, int64_t M, int64_t K, int64_t C, hipStream_t stream) {
     SGC_REQUIRE(X && W && Y, SGC_EINVAL, "linear: null pointer");
@@ -94,6 +333,38 @@ int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *
         const float *Wc = W + c0 * K;
         const float *bc = b ? b + c0 : nullptr;
         float *Yc = Y + c0;
+        size_t lds = 0;
+        const bool stream_ok = stream_fits(M, K, ldx, nt, X, &lds);
+        if (g_linear_kernel >= 3) {  // diagnostics: NT = 3, 8-B rows only
+            SGC_REQUIRE(stream_ok && nt == 3, SGC_EINVAL, "linear: diagnostic kernel needs NT = 3");
+            const int Kp = (int)((K + 31) / 32 * 32);
+            hipError_t e = g_linear_kernel == 3
+                ? launch_stream<2, 3, 1>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream)
+                : launch_stream<2, 3, 2>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream);
+            SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear launch failed: %s", hipGetErrorString(e));
+            continue;
+        }
+        if (g_linear_kernel == 2 || (g_linear_kernel == 0 && stream_ok && M >= 4096)) {
+            SGC_REQUIRE(stream_ok, SGC_EINVAL, "linear: streaming kernel preconditions not met");
+            const int Kp = (int)((K + 31) / 32 * 32);
+            const bool v4 = ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0;
+            hipError_t e;
+#define SGC_STREAM(VV)                                                                         \
+    switch (nt) {                                                                              \
+        case 1: e = launch_stream<VV, 1>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream); break; \
+        case 2: e = launch_stream<VV, 2>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream); break; \
+        case 3: e = launch_stream<VV, 3>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream); break; \
+        default: e = launch_stream<VV, 4>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream); break; \
+    }
+            if (v4) {
+                SGC_STREAM(4)
+            } else {
+                SGC_STREAM(2)
+            }
+#undef SGC_STREAM
+            SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear launch failed: %s", hipGetErrorString(e));
+            continue;
+        }
         int V = 1;
         for (int v : {4, 2}) {
             // natural alignment of every vector load (the k >= K tail is masked)

@@ -673,17 +673,36 @@ __device__ __forceinline__ void row_quadsT_pipe(const int *__restrict__ col,
 #ifndef SGC_HEAVY_VEC
 #define SGC_HEAVY_VEC 2
 #endif
-template <int V, int C, int U, int UH>
+template <int HC, int NL>
+__device__ __forceinline__ void hub_body(
+    int bid, const int *__restrict__ row_ptr, const int *__restrict__ col,
+    const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
+    float *__restrict__ Y, int64_t ldy, int row_begin, int F, const int *__restrict__ hub_rows,
+    int n_chunks, int accum);
+
+// HF > 0: the serial hub rows fused into the launch (as spmm_rows_kernel's HF).
+template <int V, int C, int U, int UH, int HF = 0>
 __global__ __launch_bounds__(256) void spmm_csr_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
     int row_begin, int n_rows, int F, const int *__restrict__ heavy_rows, int n_heavy,
-    int heavy_threshold, int accum, int heavy_pairs) {
+    int heavy_threshold, int accum, int heavy_pairs, const int *__restrict__ hub_rows = nullptr,
+    int hub_chunks = 0, int n_hub_blocks = 0) {
     constexpr int VH = (SGC_HEAVY_VEC < V) ? SGC_HEAVY_VEC : V;  // heavy lanes' vector width
     constexpr int kSub = C * V / VH;  // 64*VH-float sub-chunks per slice (heavy items)
+    int bx = (int)blockIdx.x;
+    if constexpr (HF > 0) {
+        if (bx < n_hub_blocks) {  // block-uniform
+            if (blockIdx.y == 0)
+                hub_body<HF, 3>(bx, row_ptr, col, val, X, ldx, Y, ldy, row_begin, F, hub_rows,
+                                hub_chunks, accum);
+            return;
+        }
+        bx -= n_hub_blocks;
+    }
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = __builtin_amdgcn_readfirstlane(
-        (int)(blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave)));
+        (int)(bx * (blockDim.x / kWave) + (threadIdx.x / kWave)));
     const int slice = blockIdx.y;
     const int n_heavy_items = n_heavy * kSub;
     if (wave < n_heavy_items) {
@@ -752,13 +771,33 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
 // slower on a 76-float slice, profiles/r02/packed_sweep.log).
 constexpr int kRowsU = 4;  // nonzeros per row per step (one b128 (col, val) read each)
 
-template <int LB, int VH, int UH, bool O32, int QV>
+
+// HF > 0: the fused rows + hub launch (small graphs whose hub chains are
+// short, SGC_SPMM_HUB_SERIAL): the first n_hub_blocks workgroups of slice 0
+// each run one (hub row, HF-float chunk) item of the hub kernel with three
+// loader waves and the chain wave (hub_body<HF, 3>, the rows kernel's 256
+// threads), every other workgroup the rows kernel's work -- one launch, so
+// the hub chains run beside the light rows with no second launch and no
+// cross-stream fork / join (Pubmed shape: the serial hub kernel added its
+// whole 15 us chain to every hop).
+template <int LB, int VH, int UH, bool O32, int QV, int HF = 0>
 __global__ __launch_bounds__(256) void spmm_rows_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy,
     int row_begin, int n_rows, int F, int F_load, int LR, int vec_store, int n_sub,
     const int *__restrict__ heavy_rows, int n_heavy, int heavy_threshold, int accum,
-    const int *__restrict__ light_rows, int heavy_pairs) {
+    const int *__restrict__ light_rows, int heavy_pairs, const int *__restrict__ hub_rows = nullptr,
+    int hub_chunks = 0, int n_hub_blocks = 0) {
+    int bx = (int)blockIdx.x;
+    if constexpr (HF > 0) {
+        if (bx < n_hub_blocks) {  // block-uniform
+            if (blockIdx.y == 0)
+                hub_body<HF, 3>(bx, row_ptr, col, val, X, ldx, Y, ldy, row_begin, F, hub_rows,
+                                hub_chunks, accum);
+            return;
+        }
+        bx -= n_hub_blocks;
+    }
     constexpr int V = 4, U = kRowsU < LB / 2 ? kRowsU : LB / 2;
     constexpr int kSteps = LB / U;  // steps per LDS block
     static_assert(kSteps >= 2 && kSteps % 2 == 0, "bad block");
@@ -768,7 +807,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     __shared__ __attribute__((aligned(16))) float s_val[kBlock / kWave][2][kWave];
     const int lane = threadIdx.x & (kWave - 1);
     const int wl = threadIdx.x / kWave;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (kBlock / kWave) + wl));
+    const int wave = __builtin_amdgcn_readfirstlane((int)(bx * (kBlock / kWave) + wl));
     const int slice = blockIdx.y;
     const int R = kWave / LR;  // rows per wave (uniform)
     const int n_heavy_items = n_heavy * n_sub;
@@ -1016,7 +1055,7 @@ constexpr int kStampRounds = 4096;
 __device__ unsigned long long g_hub_stamp[5][kStampRounds];
 #define HUB_STAMP(slot, r)                                                            \
     do {                                                                              \
-        if (blockIdx.x == 0 && lane == 0 && (r) < kStampRounds)                       \
+        if (bid == 0 && lane == 0 && (r) < kStampRounds)                              \
             g_hub_stamp[slot][r] = __builtin_amdgcn_s_memtime();                      \
     } while (0)
 #else
@@ -1166,11 +1205,15 @@ __device__ __forceinline__ void hub_chain_dpp(float &acc, uint32_t xa, uint32_t 
 // NL loader waves + the chain wave per workgroup: 15 (1024 threads, ~133 KB
 // of LDS: one workgroup per CU) or 7 (512 threads, ~68 KB: two per CU, half
 // the CU held per hub chain; sgc_set_tuning("hub_loaders")).
+// The body of one hub work item (hub row h, feature chunk c of block `bid`),
+// shared by spmm_hub_kernel and the fused rows + hub launch of
+// spmm_rows_kernel (HF > 0: NL = 3, the rows kernel's 256 threads).
 template <int HC, int NL>
-__global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
-    const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
-    const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy, int row_begin,
-    int F, const int *__restrict__ hub_rows, int n_chunks, int accum) {
+__device__ __forceinline__ void hub_body(
+    int bid, const int *__restrict__ row_ptr, const int *__restrict__ col,
+    const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
+    float *__restrict__ Y, int64_t ldy, int row_begin, int F, const int *__restrict__ hub_rows,
+    int n_chunks, int accum) {
     using Sh = HubShape<HC, NL>;
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) float gxT[2][HC * Sh::kStride];  // 2 x 66.5 KB
@@ -1181,8 +1224,8 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
     // wave 0 runs the chain, waves 1..NL load (loader index li)
     const bool loader = w > 0;
     const int li = w - 1;
-    const int h = blockIdx.x / n_chunks;
-    const int c = blockIdx.x - h * n_chunks;
+    const int h = bid / n_chunks;
+    const int c = bid - h * n_chunks;
     const int row = hub_rows[h];
     const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
     const int fl = lane & (HC - 1);  // feature within the chunk
@@ -1239,7 +1282,7 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
         if (n_round > 0) store(0, 0);
     }
 #if SGC_HUB_STAMPS
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (bid == 0 && threadIdx.x == 0) {
         g_hub_stamp[4][0] = __builtin_amdgcn_s_memtime();
         g_hub_stamp[4][1] = __builtin_amdgcn_s_memrealtime();
     }
@@ -1292,11 +1335,20 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
     }
     if (w == 0 && seg == 0 && f < F) Y[(int64_t)(row - row_begin) * ldy + f] = acc;
 #if SGC_HUB_STAMPS
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (bid == 0 && threadIdx.x == 0) {
         g_hub_stamp[4][2] = __builtin_amdgcn_s_memtime();
         g_hub_stamp[4][3] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
+}
+
+template <int HC, int NL>
+__global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
+    const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
+    const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy, int row_begin,
+    int F, const int *__restrict__ hub_rows, int n_chunks, int accum) {
+    hub_body<HC, NL>((int)blockIdx.x, row_ptr, col, val, X, ldx, Y, ldy, row_begin, F, hub_rows,
+                     n_chunks, accum);
 }
 
 namespace {
@@ -1319,6 +1371,9 @@ struct LaunchArgs {
     hipStream_t stream;
     const int *light_rows;  // SGC_SPMM_LIGHT_ORDER: the light rows in processing order, or null
     int n_light;
+    // fused rows + hub launch (spmm_rows_kernel HF = 32): the hub rows and items
+    const int *hub_rows = nullptr;
+    int hub_chunks = 0, n_hub_blocks = 0;
 };
 
 // A side stream + fork/join events per (device, caller's stream) for the
@@ -1364,7 +1419,7 @@ hipError_t side_stream(SideStream **out, hipStream_t caller) {
 // graph capture.
 struct TimedLaunch {
     hipEvent_t l0 = nullptr, l1 = nullptr, h0 = nullptr, h1 = nullptr;
-    int kernel = -1;      // light kernel: 0 spmm_csr_kernel, 1 spmm_rows_kernel, -1 none
+    int kernel = -1;  // light kernel: 0 spmm_csr_kernel, 1 spmm_rows_kernel, 2 / 3 the same with the hub rows fused, -1 none
     bool serial = false;  // hub kernel ran before the light kernel on the same stream
     bool hub_first = false;  // concurrent: hub kernel on the caller's stream, light on the side
 };
@@ -1444,19 +1499,21 @@ static int g_heavy_pairs = 29;
 // 0.109 ms.
 constexpr int kChunksPipe2Rows = 1 << 20;
 
-template <int V, int C>
+template <int V, int C, int HF = 0>
 hipError_t launch_vc(const LaunchArgs &a) {
     constexpr int U0 = (C * V >= 16) ? 2 : (C * V >= 8) ? 4 : 8;
     constexpr int U = U0;
     constexpr int UH = kHeavyU;
     constexpr int VH = (SGC_HEAVY_VEC < V) ? SGC_HEAVY_VEC : V;
     const int64_t waves = (int64_t)a.n_heavy * (C * V / VH) + a.n_rows;
-    const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock + (HF ? a.n_hub_blocks : 0);
+    if (blocks >= INT32_MAX) return hipErrorInvalidValue;
     dim3 grid((unsigned)blocks, (unsigned)a.slices);
-    hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH>), grid, dim3(kBlock), 0, a.stream,
+    hipLaunchKernelGGL((spmm_csr_kernel<V, C, U, UH, HF>), grid, dim3(kBlock), 0, a.stream,
                        a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin, a.n_rows,
                        a.F, a.heavy_rows, a.n_heavy, a.heavy_threshold, a.accum,
-                       ((g_heavy_pairs >> 1) & 1) | (a.n_rows >= kChunksPipe2Rows ? 2 : 0));
+                       ((g_heavy_pairs >> 1) & 1) | (a.n_rows >= kChunksPipe2Rows ? 2 : 0),
+                       a.hub_rows, a.hub_chunks, HF ? a.n_hub_blocks : 0);
     return hipGetLastError();
 }
 
@@ -1491,7 +1548,7 @@ static int g_rows_per_wave = 0;
 // launches (Pubmed shape, F = 500) stay latency-bound on the one-row kernel.
 constexpr int64_t kWideRowsMin = 65536;
 
-template <int LB, int VH, bool O32, int QV>
+template <int LB, int VH, bool O32, int QV, int HF = 0>
 hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     const int R = kWave / LR, SW = LR * 4;
     // each light row stages LB (col, val) pairs in its wave's 64-entry LDS block
@@ -1506,12 +1563,14 @@ hipError_t launch_rows(const LaunchArgs &a, int F_load, int LR, int vec_store) {
     // light order exactly the light rows
     const int n_light_items = a.light_rows ? a.n_light : a.n_rows;
     const int64_t waves = heavy_waves + (n_light_items + R - 1) / R;
-    const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int64_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock + (HF ? a.n_hub_blocks : 0);
+    if (blocks >= INT32_MAX) return hipErrorInvalidValue;
     dim3 grid((unsigned)blocks, (unsigned)slices);
-    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU, O32, QV>), grid, dim3(kBlock), 0, a.stream,
-                       a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
+    hipLaunchKernelGGL((spmm_rows_kernel<LB, VH, kHeavyU, O32, QV, HF>), grid, dim3(kBlock), 0,
+                       a.stream, a.row_ptr, a.col, a.val, a.X, a.ldx, a.Y, a.ldy, a.row_begin,
                        n_light_items, a.F, F_load, LR, vec_store, n_sub, a.heavy_rows, a.n_heavy,
-                       a.heavy_threshold, a.accum, a.light_rows, g_heavy_pairs & 17);
+                       a.heavy_threshold, a.accum, a.light_rows, g_heavy_pairs & 17, a.hub_rows,
+                       a.hub_chunks, HF ? a.n_hub_blocks : 0);
     return hipGetLastError();
 }
 
@@ -1558,6 +1617,11 @@ static int g_hub_stream = 0;
 // Loader waves per hub workgroup: 15 or 7 (spmm_hub_kernel).  Set through
 // sgc_set_tuning("hub_loaders").
 static int g_hub_loaders = 15;
+// Serial hub rows (SGC_SPMM_HUB_SERIAL) inside the multi-row kernel's launch
+// (spmm_rows_kernel HF = 32) instead of a hub kernel launch before it: 1 = on
+// where the launch takes the multi-row kernel on 128-B aligned X rows.  Set
+// through sgc_set_tuning("hub_fuse").
+static int g_hub_fuse = 1;
 
 int set_tuning(const char *key, int64_t value) {
     SGC_REQUIRE(key, SGC_EINVAL, "set_tuning: null key");
@@ -1575,6 +1639,11 @@ int set_tuning(const char *key, int64_t value) {
     if (std::string(key) == "hub_loaders") {
         SGC_REQUIRE(value == 7 || value == 15, SGC_EINVAL, "hub_loaders must be 7 or 15");
         g_hub_loaders = (int)value;
+        return SGC_OK;
+    }
+    if (std::string(key) == "hub_fuse") {
+        SGC_REQUIRE(value == 0 || value == 1, SGC_EINVAL, "hub_fuse must be 0 or 1");
+        g_hub_fuse = (int)value;
         return SGC_OK;
     }
     if (std::string(key) == "hub_stream") {
@@ -1598,6 +1667,11 @@ int set_tuning(const char *key, int64_t value) {
         g_tile_buffers = (int)value;
         return SGC_OK;
     }
+    if (std::string(key) == "linear_kernel") {
+        SGC_REQUIRE(value >= 0 && value <= 4, SGC_EINVAL, "linear_kernel must be 0..4");
+        g_linear_kernel = (int)value;
+        return SGC_OK;
+    }
     if (std::string(key) == "max_vec") {
         SGC_REQUIRE(value == 1 || value == 2 || value == 4, SGC_EINVAL, "max_vec must be 1, 2 or 4");
         g_max_vec = (int)value;
@@ -1615,7 +1689,9 @@ int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "hub_chunk") return g_hub_chunk;
     if (key && std::string(key) == "hub_stream") return g_hub_stream;
     if (key && std::string(key) == "hub_loaders") return g_hub_loaders;
+    if (key && std::string(key) == "hub_fuse") return g_hub_fuse;
     if (key && std::string(key) == "tile_buffers") return g_tile_buffers;
+    if (key && std::string(key) == "linear_kernel") return g_linear_kernel;
     return -1;
 }
 
@@ -1668,39 +1744,16 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
     if (timing) timed_guard.tl = &tl;
     SideJoin side_join;
     hipStream_t light_stream = stream;
-    if (n_hub > 0) {
-        // hub rows (the heaviest n_hub of the plan) run beside the light
-        // kernel (g_hub_stream); 32-feature chunks spread a hub over more CUs; measured faster up to
-        // F = 160 and slower from F = 320 (scripts/sweep_narrow.py), and they
-        // need 128-B aligned rows to stay one line per segment.
-        const bool lines = ldx % 32 == 0 && reinterpret_cast<uintptr_t>(X) % 128 == 0;
-        const int hc = g_hub_chunk ? g_hub_chunk : (lines && F <= 192 ? 32 : 64);
+    // hub kernel launch (on the caller's stream) of the n_hub rows at hub_rows
+    const bool lines = ldx % 32 == 0 && reinterpret_cast<uintptr_t>(X) % 128 == 0;
+    const int32_t *hub_rows = heavy_rows;
+    auto launch_hub = [&](hipStream_t hs, int hc) -> hipError_t {
         const int n_chunks = (int)((F + hc - 1) / hc);
-        SGC_REQUIRE(n_hub * n_chunks < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many hub items");
-        const hipStream_t hs = stream;  // always the caller's stream
-        const bool serial =
-            g_hub_stream == 2 || (g_hub_stream == 0 && (flags & SGC_SPMM_HUB_SERIAL));
-        if (!hub_only && !serial) {
-            SGC_HIP_CHECK(side_stream(&side, stream));
-            side_lock = std::unique_lock<std::mutex>(side->mu);
-            SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
-            SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
-            side_join.side = side;  // from here on every exit joins
-            side_join.stream = stream;
-            light_stream = side->s;  // the hub kernel stays on the caller's stream
-            tl.hub_first = true;
-        }
-        if (timing) {
-            SGC_HIP_CHECK(pooled_event(&tl.h0));
-            SGC_HIP_CHECK(pooled_event(&tl.h1));
-            SGC_HIP_CHECK(hipEventRecord(tl.h0, hs));
-            tl.serial = hs == light_stream;
-        }
         const dim3 hub_grid((unsigned)(n_hub * n_chunks));
 #define SGC_LAUNCH_HUB(HCV, NLV)                                                             \
     hipLaunchKernelGGL((spmm_hub_kernel<HCV, NLV>), hub_grid, dim3(64 * (NLV + 1)), 0, hs,   \
                        row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)F,        \
-                       heavy_rows, n_chunks, accum)
+                       hub_rows, n_chunks, accum)
         if (hc == 32) {
             if (g_hub_loaders == 7) SGC_LAUNCH_HUB(32, 7);
             else SGC_LAUNCH_HUB(32, 15);
@@ -1709,8 +1762,42 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             else SGC_LAUNCH_HUB(64, 15);
         }
 #undef SGC_LAUNCH_HUB
-        SGC_HIP_CHECK(hipGetLastError());
-        if (timing) SGC_HIP_CHECK(hipEventRecord(tl.h1, hs));
+        return hipGetLastError();
+    };
+    // 32-feature chunks spread a hub over more CUs; measured faster up to
+    // F = 160 and slower from F = 320 (scripts/sweep_narrow.py), and they
+    // need 128-B aligned rows to stay one line per segment.
+    const int hub_hc = g_hub_chunk ? g_hub_chunk : (lines && F <= 192 ? 32 : 64);
+    bool hub_deferred = false;  // serial hub rows left for the fused launch (or just before the light kernel)
+    if (n_hub > 0) {
+        // hub rows (the heaviest n_hub of the plan) run beside the light
+        // kernel (g_hub_stream)
+        SGC_REQUIRE(n_hub * ((F + 31) / 32) < (int64_t)INT32_MAX, SGC_ERANGE,
+                    "spmm: too many hub items");
+        const hipStream_t hs = stream;  // always the caller's stream
+        const bool serial =
+            g_hub_stream == 2 || (g_hub_stream == 0 && (flags & SGC_SPMM_HUB_SERIAL));
+        hub_deferred = serial && !hub_only && g_hub_fuse && lines && g_hub_chunk == 0;
+        if (!hub_deferred) {
+            if (!hub_only && !serial) {
+                SGC_HIP_CHECK(side_stream(&side, stream));
+                side_lock = std::unique_lock<std::mutex>(side->mu);
+                SGC_HIP_CHECK(hipEventRecord(side->fork, stream));
+                SGC_HIP_CHECK(hipStreamWaitEvent(side->s, side->fork, 0));
+                side_join.side = side;  // from here on every exit joins
+                side_join.stream = stream;
+                light_stream = side->s;  // the hub kernel stays on the caller's stream
+                tl.hub_first = true;
+            }
+            if (timing) {
+                SGC_HIP_CHECK(pooled_event(&tl.h0));
+                SGC_HIP_CHECK(pooled_event(&tl.h1));
+                SGC_HIP_CHECK(hipEventRecord(tl.h0, hs));
+                tl.serial = hs == light_stream;
+            }
+            SGC_HIP_CHECK(launch_hub(hs, hub_hc));
+            if (timing) SGC_HIP_CHECK(hipEventRecord(tl.h1, hs));
+        }
         heavy_rows += n_hub;
         n_heavy -= n_hub;
         if (hub_only) {
@@ -1724,6 +1811,19 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             return SGC_OK;
         }
     }
+    // a deferred hub launch that the fused kernel does not take runs here,
+    // serially before the light kernel, as it would have
+    auto hub_before_light = [&]() -> int {
+        if (timing) {
+            SGC_HIP_CHECK(pooled_event(&tl.h0));
+            SGC_HIP_CHECK(pooled_event(&tl.h1));
+            SGC_HIP_CHECK(hipEventRecord(tl.h0, stream));
+            tl.serial = true;
+        }
+        SGC_HIP_CHECK(launch_hub(stream, hub_hc));
+        if (timing) SGC_HIP_CHECK(hipEventRecord(tl.h1, stream));
+        return SGC_OK;
+    };
 
     LaunchArgs a{row_ptr, col_idx, val, X, ldx, Y, ldy, (int)row_begin, (int)n_rows, (int)F,
                  heavy_rows, (int)n_heavy, heavy_threshold, 0, accum, light_stream};
@@ -1768,11 +1868,23 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
                          ya % 8 == 0 && (!multi || SW % (kWave * 2) == 0);
         SGC_REQUIRE(n_heavy * 8 + n_rows < (int64_t)INT32_MAX, SGC_ERANGE,
                     "spmm: too many work items");
+        // the fused hub items need the 256-thread multi-row kernel with
+        // 16-B lanes over whole slices (LR >= 16, two-float heavy sub-chunks)
+        const bool fused = hub_deferred && LR >= 16 && vh2 && F4 > 64;
+        if (hub_deferred && !fused) {
+            const int rc = hub_before_light();
+            if (rc != SGC_OK) return rc;
+        }
+        if (fused) {
+            a.hub_rows = hub_rows;
+            a.hub_chunks = (int)((F + 31) / 32);
+            a.n_hub_blocks = (int)(n_hub * a.hub_chunks);
+        }
         if (timing) {
             SGC_HIP_CHECK(pooled_event(&tl.l0));
             SGC_HIP_CHECK(pooled_event(&tl.l1));
             SGC_HIP_CHECK(hipEventRecord(tl.l0, light_stream));
-            tl.kernel = 1;
+            tl.kernel = fused ? 2 : 1;
         }
         // 32-bit row offsets (one full-rate 24-bit multiply per gathered row)
         // when the caller vouches that X spans < 4 GiB and has < 2^24 rows
@@ -1795,6 +1907,9 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
             e = SGC_ROWS(8, 2, 2);
         else if (qv == 1)
             e = SGC_ROWS(8, 2, 1);
+        else if (fused)
+            e = o32 ? launch_rows<16, 2, true, 0, 32>(a, (int)F4, LR, vec_store)
+                    : launch_rows<16, 2, false, 0, 32>(a, (int)F4, LR, vec_store);
         else if (LR >= 16)
             e = vh2 ? SGC_ROWS(16, 2, 0) : SGC_ROWS(16, 1, 0);
         else
@@ -1813,13 +1928,26 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         SGC_REQUIRE(waves < (int64_t)INT32_MAX, SGC_ERANGE, "spmm: too many work items");
         SGC_REQUIRE(slices < 65536, SGC_ERANGE, "spmm: too many feature slices");
         a.slices = slices;
+        // the fused hub items: the 16-B-lane, one-chunk slice form (Pubmed shape)
+        const bool fused = hub_deferred && V == 4 && C == 1;
+        if (hub_deferred && !fused) {
+            const int rc = hub_before_light();
+            if (rc != SGC_OK) return rc;
+        }
+        if (fused) {
+            a.hub_rows = hub_rows;
+            a.hub_chunks = (int)((F + 31) / 32);
+            a.n_hub_blocks = (int)(n_hub * a.hub_chunks);
+        }
         if (timing) {
             SGC_HIP_CHECK(pooled_event(&tl.l0));
             SGC_HIP_CHECK(pooled_event(&tl.l1));
             SGC_HIP_CHECK(hipEventRecord(tl.l0, light_stream));
-            tl.kernel = 0;
+            tl.kernel = fused ? 3 : 0;
         }
-        if (V == 4)
+        if (fused)
+            e = launch_vc<4, 1, 32>(a);
+        else if (V == 4)
             e = dispatch_c<4, max_chunks(4)>(C, a);
         else if (V == 2)
             e = dispatch_c<2, max_chunks(2)>(C, a);

@@ -839,7 +839,8 @@ def collect_launch_timing(capacity=1 << 16):
     _lib.check(lib.sgc_timing_collect_ex(*(ctypes.cast(b, ctypes.c_void_p)
                                            for b in (light, hub, span, kind)),
                                          capacity, ctypes_byref(n)), "timing_collect_ex")
-    names = {0: "spmm_csr_kernel", 1: "spmm_rows_kernel"}
+    names = {0: "spmm_csr_kernel", 1: "spmm_rows_kernel", 2: "spmm_rows_kernel+hub (fused)",
+             3: "spmm_csr_kernel+hub (fused)"}
     k = int(n.value)
     return ([float(light[i]) for i in range(k)],
             [float(hub[i]) if hub[i] >= 0 else None for i in range(k)],

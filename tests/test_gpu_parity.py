@@ -428,15 +428,19 @@ def test_accumulate_column_block_passes(oracle, F, rows_per_wave, th, hub):
         lib.sgc_set_tuning(b"rows_per_wave", 0)
 
 
+@pytest.mark.parametrize("fuse", [0, 1])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_hub_stream_modes_bit_exact(tiny_cases, oracle, mode):
+def test_hub_stream_modes_bit_exact(tiny_cases, oracle, mode, fuse):
     """Hub kernel beside the light kernel (side stream, fork/join), in line
     before it (SGC_SPMM_HUB_SERIAL / hub_stream=2) or per the plan's longest
-    hub row (default): the same bits."""
+    hub row (default); serial hub rows inside the multi-row kernel's launch
+    (hub_fuse 1: F = 130 in 128-B rows) or as their own launch: the same
+    bits."""
     from sgc_amd import _lib
     from sgc_amd.propagate import DeviceCSR, HUB_SERIAL_MAX_DEGREE, propagate
     lib = _lib.load()
     _lib.check(lib.sgc_set_tuning(b"hub_stream", mode), "set_tuning")
+    _lib.check(lib.sgc_set_tuning(b"hub_fuse", fuse), "set_tuning")
     try:
         for name in ("hub1000_F130", "hub1000_F65", "norm_n48_F602"):
             c = tiny_cases[name]
@@ -448,9 +452,10 @@ def test_hub_stream_modes_bit_exact(tiny_cases, oracle, mode):
                 assert 0 < pl.max_hub_degree <= HUB_SERIAL_MAX_DEGREE
             out = propagate(csr, torch.from_numpy(c["X"]).to(DEV), 2, threshold=7, hub_threshold=7)
             torch.cuda.synchronize()
-            assert bits_equal(out.cpu().numpy(), c["Y2"]), (name, mode)
+            assert bits_equal(out.cpu().numpy(), c["Y2"]), (name, mode, fuse)
     finally:
         lib.sgc_set_tuning(b"hub_stream", 0)
+        lib.sgc_set_tuning(b"hub_fuse", 1)
 
 
 def test_accumulate_requires_out():
@@ -553,6 +558,36 @@ def test_linear_tile_edges(tile_buffers, M, K, C, ld_extra):
             torch.testing.assert_close(logits.cpu().double(), ref, rtol=1e-5, atol=tol)
     finally:
         lib.sgc_set_tuning(b"tile_buffers", 1)
+
+
+@pytest.mark.parametrize("M,K,C,ld_extra", [(129, 602, 41, 6), (300, 33, 17, 1), (257, 31, 3, 1),
+                                            (128, 64, 64, 32), (1, 1, 1, 1), (500, 576, 70, 2),
+                                            (70000, 602, 41, 0), (66000, 100, 48, 4)])
+def test_linear_stream_edges(M, K, C, ld_extra):
+    """The streaming forward (linear_stream_kernel, forced): W^T in LDS, X
+    streamed per 16-row tile with b128 (ld % 4 == 0) or b64 loads (ld = 602,
+    the Reddit-train layout); rows past M read zeros, the last chunk's k >= K
+    are zeroed (X holds infinities there); M = 70,000 / 66,000 give waves
+    more than one tile, so the chunk stream crosses tile boundaries."""
+    from sgc_amd import _lib
+    from sgc_amd.propagate import linear
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + K + C)
+    Xf = torch.full((M, K + ld_extra), float("inf"))
+    Xf[:, :K] = torch.randn((M, K), generator=g)
+    W = torch.randn((C, K), generator=g) * 0.05
+    b = torch.randn(C, generator=g)
+    ref = torch.nn.functional.linear(Xf[:, :K].double(), W.double(), b.double())
+    tol = 1e-5 * max(1.0, ref.abs().max().item())
+    _lib.check(lib.sgc_set_tuning(b"linear_kernel", 2), "set_tuning")
+    try:
+        Xd = Xf.to(DEV)[:, :K]
+        Y = linear(Xd, W.to(DEV), b.to(DEV)).cpu().double()
+        torch.testing.assert_close(Y, ref, rtol=1e-5, atol=tol)
+        Yn = linear(Xd, W.to(DEV), None).cpu().double()
+        torch.testing.assert_close(Yn, ref - b.double(), rtol=1e-5, atol=tol)
+    finally:
+        lib.sgc_set_tuning(b"linear_kernel", 0)
 
 
 def test_sgc_model_autograd_matches_torch():
