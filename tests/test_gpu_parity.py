@@ -492,23 +492,33 @@ def test_fused_xent_rejects_bad_labels():
             linear_xent(X, W, b, y)
 
 
-def test_kernel_timing_hooks(tiny_cases):
-    """sgc_timing_*: one (light, hub) pair per SpMM launch, hub None without hubs."""
+@pytest.mark.parametrize("fuse", [0, 1])
+def test_kernel_timing_hooks(tiny_cases, fuse):
+    """sgc_timing_*: one (light, hub) pair per SpMM launch, hub None without
+    hubs -- and None as well when the (serial) hub rows ran inside the light
+    launch (hub_fuse 1: the light kernel's time covers them)."""
+    from sgc_amd import _lib
     from sgc_amd.propagate import (DeviceCSR, collect_kernel_timing, kernel_timing,
                                    propagate)
+    lib = _lib.load()
     c = tiny_cases["hub1000_F130"]
     csr = DeviceCSR.from_torch(coo_cuda(c))
     X = torch.from_numpy(c["X"]).to(DEV)
     collect_kernel_timing()
+    _lib.check(lib.sgc_set_tuning(b"hub_fuse", fuse), "set_tuning")
     kernel_timing(True)
     try:
         out = propagate(csr, X, 2, threshold=3, hub_threshold=5)
         propagate(csr, X, 1, threshold=10**9, hub_threshold=10**9)
     finally:
         kernel_timing(False)
+        lib.sgc_set_tuning(b"hub_fuse", 1)
     light, hub = collect_kernel_timing()
     assert len(light) == 3 and all(t > 0 for t in light)
-    assert hub[0] > 0 and hub[1] > 0 and hub[2] is None
+    if fuse:  # hop 2 reads X_1 in the engine's 128-B rows: fused (hop 1 reads X_0 as given)
+        assert hub[1] is None and hub[2] is None
+    else:
+        assert hub[0] > 0 and hub[1] > 0 and hub[2] is None
     assert bits_equal(out.cpu().numpy(), c["Y2"])
     assert collect_kernel_timing() == ([], [])
 
