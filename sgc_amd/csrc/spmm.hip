@@ -1618,9 +1618,10 @@ static int g_hub_stream = 0;
 // sgc_set_tuning("hub_loaders").
 static int g_hub_loaders = 15;
 // Serial hub rows (SGC_SPMM_HUB_SERIAL) inside the multi-row kernel's launch
-// (spmm_rows_kernel HF = 32) instead of a hub kernel launch before it: 1 = on
-// where the launch takes the multi-row kernel on 128-B aligned X rows.  Set
-// through sgc_set_tuning("hub_fuse").
+// (spmm_rows_kernel / spmm_csr_kernel HF = 32) instead of a hub kernel launch
+// before it: 1 = on where the launch takes the multi-row kernel over whole
+// 16-B-lane slices or the one-chunk csr kernel.  Set through
+// sgc_set_tuning("hub_fuse").
 static int g_hub_fuse = 1;
 
 int set_tuning(const char *key, int64_t value) {
@@ -1777,7 +1778,8 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
         const hipStream_t hs = stream;  // always the caller's stream
         const bool serial =
             g_hub_stream == 2 || (g_hub_stream == 0 && (flags & SGC_SPMM_HUB_SERIAL));
-        hub_deferred = serial && !hub_only && g_hub_fuse && lines && g_hub_chunk == 0;
+        // (the fused items read floats one at a time: any row alignment)
+        hub_deferred = serial && !hub_only && g_hub_fuse && g_hub_chunk == 0;
         if (!hub_deferred) {
             if (!hub_only && !serial) {
                 SGC_HIP_CHECK(side_stream(&side, stream));

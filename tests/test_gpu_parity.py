@@ -515,7 +515,7 @@ def test_kernel_timing_hooks(tiny_cases, fuse):
         lib.sgc_set_tuning(b"hub_fuse", 1)
     light, hub = collect_kernel_timing()
     assert len(light) == 3 and all(t > 0 for t in light)
-    if fuse:  # hop 2 reads X_1 in the engine's 128-B rows: fused (hop 1 reads X_0 as given)
+    if fuse:  # hop 2 (X_1 in the engine's 16-B-lane rows) fused; hop 1 reads X_0 (F = 130) with 8-B lanes
         assert hub[1] is None and hub[2] is None
     else:
         assert hub[0] > 0 and hub[1] > 0 and hub[2] is None
