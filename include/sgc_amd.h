@@ -60,7 +60,21 @@ const char *sgc_last_error(void);
  *                   (0 = default, auto; 2 = 32 lanes x 4 floats per row; 4 =
  *                   16 lanes; 1 = one row per wave with the slice_floats /
  *                   max_vec scheme);
- *   "hub_loaders":  loader waves per hub workgroup, 15 (default) or 7.
+ *   "hub_loaders":  loader waves per hub workgroup, 15 (default) or 7;
+ *   "hub_fuse":     1 (default) = serial hub rows (SGC_SPMM_HUB_SERIAL) run as
+ *                   the first workgroups of the light kernel's own launch
+ *                   (three loader waves + the chain wave each) where that is
+ *                   the multi-row kernel over 16-B-lane slices or the
+ *                   one-chunk csr kernel; 0 = their own launch before it;
+ *   "heavy_pairs":  heavy-row load forms, a bit mask (default 29): 1 pairs in
+ *                   the multi-row kernel, 2 in the one-row kernel, 4 four
+ *                   nonzeros per load up to 32 floats, 8 the same transposed
+ *                   at 33..64 floats, 16 the pairs transposed;
+ *   "tile_buffers": classifier LDS tile images, 1 (default) or 2;
+ *   "linear_kernel": classifier forward, 0 = auto (the streaming kernel where
+ *                   W^T fits LDS and M >= 4096), 1 = LDS tile, 2 = streaming
+ *                   (3 / 4: its diagnostic forms -- loads only / MFMAs only --
+ *                   whose results are wrong by design).
  * sgc_get_tuning returns -1 for an unknown key. */
 int sgc_set_tuning(const char *key, int64_t value);
 int64_t sgc_get_tuning(const char *key);

@@ -11,11 +11,11 @@ ranks' slots hold zeros), so what is timed is the rank's compute: block
 copies, the K main hops over all rows, the K tail hops over its rows, the
 last hop's unpack.  The exchanges are then modelled at a stated link rate (one
 xGMI link per GPU pair, --link-gbps each way, a rank's ingress (P-1) links):
-  * the tail gathers of hops 1..K-1 ride under the main launches that follow
-    them (the per-rank timeline below adds whatever the main hop does not
-    cover);
+  * each hop's tail gather rides under that hop's main launch (the tail
+    launch and its gather run on the tail stream beside it; the model adds
+    whatever the main hop does not cover);
   * sharded output: the main blocks' all-to-all ((P-1)/P of the rank's rows x
-    W floats) and the last tail gather after the last hop;
+    W floats) after the last hop;
   * replicated output (the public sgc_precompute): every rank receives
     (P-1)/P of X_K -- modelled as after the last hop, no overlap credited.
 One JSON line per rank and a summary per P.
@@ -121,11 +121,11 @@ def main():
                                 args.reps)
             gather_b = (P - 1) * shard.block * ldt * 4
             t_gather = gather_b / ingress * 1e3
-            # exposed part of a between-hop gather: what the next main hop
-            # does not cover
-            exposed = (K - 1) * max(0.0, t_gather - t_main)
+            # exposed part of each tail gather: what the main hop running
+            # beside it (the same hop's, on the main stream) does not cover
+            exposed = K * max(0.0, t_gather - t_main)
             a2a_b = (P - 1) * Bn * max(W, 1) * 4
-            sharded = t_sh + exposed + (a2a_b / ingress * 1e3) + t_gather
+            sharded = t_sh + exposed + (a2a_b / ingress * 1e3)
             rep_b = (P - 1) / P * n * F * 4
             replicated = t_rep + exposed + rep_b / ingress * 1e3
             rec = {"case": "rank", "P": P, "rank": p, "main_floats": w, "tail_floats": wt,
@@ -149,9 +149,9 @@ def main():
                           "projected_replicated_speedup": t1 / pr,
                           "link_GBps_each_way": args.link_gbps,
                           "assumption": "one xGMI link per GPU pair at link_GBps each way; "
-                                        "compute measured on one GPU per rank; between-hop "
-                                        "tail gathers under the next main hop; last-hop "
-                                        "exchanges after it"}), flush=True)
+                                        "compute measured on one GPU per rank; each tail "
+                                        "gather under its hop's main launch; the main "
+                                        "blocks' exchange after the last hop"}), flush=True)
 
 
 if __name__ == "__main__":
