@@ -439,7 +439,9 @@ def _line_worker(rank, world, port, case, K, result_q, chunks, staging, output, 
     (3, "norm_n48_F65", 2, 3, False, "replicated", "nnz"),    # a line each (the last 1 float), no tail
     (4, "raw_unsorted_dups_F7", 3, 5, False, "sharded", "nnz"),  # all tail
     (2, "isolated_F17", 1, 1, True, "replicated", "nnz"),
-    (2, "norm_n48_F3", 2, 4, False, "sharded", "rows")])
+    (2, "norm_n48_F3", 2, 4, False, "sharded", "rows"),
+    (8, "norm_n48_F602", 2, 4, False, "replicated", "nnz"),    # the P = 8 layout: 64 + 90-float tail
+    (8, "hub1000_F130", 2, 3, False, "sharded", "nnz")])       # 5 lines over 8 ranks: all tail
 def test_line_partition_gloo_bit_exact(tiny_cases, oracle, world, name, K, chunks, staging,
                                        output, balance):
     """Main line blocks need no exchange; the tail's row blocks are gathered
