@@ -74,7 +74,8 @@ const char *sgc_last_error(void);
  *   "linear_kernel": classifier forward, 0 = auto (the streaming kernel where
  *                   W^T fits LDS and M >= 4096), 1 = LDS tile, 2 = streaming
  *                   (3 / 4: its diagnostic forms -- loads only / MFMAs only --
- *                   whose results are wrong by design).
+ *                   whose results are wrong by design);
+ *   "linear_ck":    k per chunk of the streaming forward, 64 (default) or 32.
  * sgc_get_tuning returns -1 for an unknown key. */
 int sgc_set_tuning(const char *key, int64_t value);
 int64_t sgc_get_tuning(const char *key);

@@ -62,6 +62,8 @@ inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s);
 extern int g_tile_buffers;
 // Classifier forward kernel (linear.hip): 0 auto, 1 LDS tile, 2 streaming.
 extern int g_linear_kernel;
+// k per chunk of the streaming classifier kernel (32 or 64).
+extern int g_linear_ck;
 
 template <int V> struct Vec { typedef float __attribute__((ext_vector_type(V))) T; };
 template <> struct Vec<1> { typedef float T; };

@@ -77,14 +77,20 @@ constexpr int kStreamWaves = 16;
 // DIAG (diagnostics only, sgc_set_tuning("linear_kernel", 3 / 4)): 1 = the
 // loads and stores without the MFMAs (the X stream's own time), 2 = the MFMAs
 // on registers without the X loads (the MFMA pipe's own time).
-template <int V, int NT, int DIAG = 0>
+// CK: k per chunk, 32 or 64 (a lane holds CK/4 k of a row per chunk; 64 = half
+// the per-chunk bookkeeping per MFMA at the same bytes in flight, two chunks
+// deep instead of four).
+template <int V, int NT, int DIAG = 0, int CK = 32>
 __global__ __launch_bounds__(64 * kStreamWaves) void linear_stream_kernel(
     const float *__restrict__ X, int64_t ldx, const float *__restrict__ W,
     const float *__restrict__ b, float *__restrict__ Y, int64_t ldy, int M, int K, int C,
     int Kp) {
     typedef float f4 __attribute__((ext_vector_type(4)));
     using VT = typename Vec<V>::T;
-    constexpr int NV = 8 / V;  // vector loads per lane per chunk
+    constexpr int E = CK / 4;              // k per lane per chunk
+    constexpr int NV = E / V;              // vector loads per lane per chunk
+    constexpr int NJ = E / 4;              // 16-B granules per lane per chunk
+    constexpr int D = CK == 32 ? kStreamDepth : kStreamDepth / 2;  // chunks in flight
     // W^T image [NT*16][S], S = K rounded up to 64 floats; the 16-B granule q
     // of row r sits at granule q ^ (r & 15) of its 64-float window, so every
     // ds_read_b128 lane group (4 x 16 lanes, MI355X_MICROARCH.md LDS table)
@@ -132,7 +138,7 @@ __global__ __launch_bounds__(64 * kStreamWaves) void linear_stream_kernel(
         const int t = (int)blockIdx.x + (int)gridDim.x * m;
         return t < n_tiles ? t : -1;
     };
-    const int NC = Kp / 32;  // chunks per tile
+    const int NC = Kp / CK;  // chunks per tile
     const auto xd = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(X), 0, (int)((int64_t)M * ldx * 4), 0x00020000);  // < 2^31
     // loader: chunk lc of tile ltile (-1: the CU's list is done)
@@ -142,13 +148,13 @@ __global__ __launch_bounds__(64 * kStreamWaves) void linear_stream_kernel(
         return (tile >= 0 && row < M) ? (uint32_t)((int64_t)row * ldx * 4) + 16u * g : kOffOOB;
     };
     uint32_t lrow = row_off(ltile);
-    VT xr[kStreamDepth][NV];
-    int stile[kStreamDepth], sc[kStreamDepth];  // each slot's (tile, chunk); tile -1 = none
+    VT xr[D][NV];
+    int stile[D], sc[D];  // each slot's (tile, chunk); tile -1 = none
     auto load = [&](int slot_) {
         stile[slot_] = ltile;
         sc[slot_] = lc;
         if (ltile < 0) return;
-        const uint32_t off = lrow + (uint32_t)lc * 128u;
+        const uint32_t off = lrow + (uint32_t)lc * (CK * 4u);
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
             if constexpr (DIAG == 2)
@@ -164,62 +170,82 @@ __global__ __launch_bounds__(64 * kStreamWaves) void linear_stream_kernel(
         }
     };
 #pragma unroll
-    for (int u = 0; u < kStreamDepth; ++u) load(u);
+    for (int u = 0; u < D; ++u) load(u);
     f32x4 acc[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
     // W operands of chunk c (granules 8c + 4h + g of rows n*16 + i, swizzled),
     // read one chunk ahead into the other register set, so the MFMAs never
     // wait for their LDS reads
-    f4 bw[2][NT][2];
-    auto read_w = [&](int c, f4 (&dst)[NT][2]) {
-        const int wbase = (c >> 1) * 64;
+    f4 bw[2][NT][NJ];
+    auto read_w = [&](int c, f4 (&dst)[NT][NJ]) {
+        const int q0 = c * E;  // the chunk's first granule... of 16 per 64-float window
+        const int wbase = (q0 >> 4) * 64;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int col = wbase + (((((c & 1) << 3) + 4 * h + g) ^ i) << 2);
+        for (int h = 0; h < NJ; ++h) {
+            const int col = wbase + (((((q0 & 15)) + 4 * h + g) ^ i) << 2);
 #pragma unroll
             for (int n = 0; n < NT; ++n)
                 dst[n][h] = *reinterpret_cast<const f4 *>(&sw[(n * 16 + i) * S + col]);
         }
     };
-    // (at NT = 4 the second set would spill at the 128-VGPR cap of 16 waves:
-    // read in place there)
-    constexpr bool kPreW = NT <= 3;
+    // (at NT = 4, or with 64-k chunks, the second set would spill at the
+    // 128-VGPR cap of 16 waves: read in place there)
+    constexpr bool kPreW = NT <= 3 && CK == 32;
     if constexpr (kPreW) read_w(sc[0], bw[0]);
-    static_assert(kStreamDepth % 2 == 0, "the W register sets alternate per slot");
+    static_assert(D % 2 == 0, "the W register sets alternate per slot");
     for (;;) {
 #pragma unroll
-        for (int u = 0; u < kStreamDepth; ++u) {
+        for (int u = 0; u < D; ++u) {
             const int tile = stile[u], c = sc[u];
             if (tile < 0) return;  // wave-uniform: the stream is in order, so all later slots are empty too
             const int cur = kPreW ? (u & 1) : 0;  // a constant after unrolling
-            const int un = (u + 1) % kStreamDepth;
+            const int un = (u + 1) % D;
             if constexpr (kPreW) {
                 if (stile[un] >= 0) read_w(sc[un], bw[cur ^ 1]);
-            } else {
+            } else if constexpr (CK == 32) {
                 read_w(c, bw[0]);
             }
-            float a[8];
+            float a[E];
 #pragma unroll
             for (int q = 0; q < NV; ++q)
 #pragma unroll
                 for (int e = 0; e < V; ++e) a[q * V + e] = lane_elem<V>(xr[u][q], e);
-            if ((c + 1) * 32 > K) {  // the ragged last chunk (uniform)
+            if ((c + 1) * CK > K) {  // the ragged last chunk (uniform)
 #pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (c * 32 + 16 * (e >> 2) + 4 * g + (e & 3) >= K) a[e] = 0.0f;
+                for (int e = 0; e < E; ++e)
+                    if (c * CK + 16 * (e >> 2) + 4 * g + (e & 3) >= K) a[e] = 0.0f;
             }
             if constexpr (DIAG == 1) {
 #pragma unroll
-                for (int kk = 0; kk < 8; ++kk)
+                for (int kk = 0; kk < E; ++kk)
                     acc[kk % NT][kk & 3] += a[kk] * bw[cur][0][0][kk & 3];
-            } else {
+            } else if constexpr (CK == 32) {
 #pragma unroll
-                for (int kk = 0; kk < 8; ++kk)
+                for (int kk = 0; kk < E; ++kk)
 #pragma unroll
                     for (int n = 0; n < NT; ++n)
                         acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(
                             a[kk], bw[cur][n][kk >> 2][kk & 3], acc[n], 0, 0, 0);
+            } else {  // 64-k chunks: W operands in two halves of two granules (registers)
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    f4 bh[NT][2];
+                    const int wbase = c * 64;
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int col = wbase + (((4 * (2 * hh + h) + g) ^ i) << 2);
+#pragma unroll
+                        for (int n = 0; n < NT; ++n)
+                            bh[n][h] = *reinterpret_cast<const f4 *>(&sw[(n * 16 + i) * S + col]);
+                    }
+#pragma unroll
+                    for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+                        for (int n = 0; n < NT; ++n)
+                            acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                                a[8 * hh + kk], bh[n][kk >> 2][kk & 3], acc[n], 0, 0, 0);
+                }
             }
             // the chunk kStreamDepth ahead into the slot just consumed
             load(u);
@@ -246,6 +272,10 @@ __global__ __launch_bounds__(64 * kStreamWaves) void linear_stream_kernel(
 // LDS tile, 2 = streaming (3 / 4: its DIAG forms, wrong results by design).
 // Set through sgc_set_tuning("linear_kernel").
 int g_linear_kernel = 0;
+// k per chunk of the streaming kernel, 32 or 64 (64: forward 0.1237-0.1238
+// vs 0.1263-0.1273 ms at the Reddit-train shape, profiles/r04/classifier_ck64_ab.log).
+// Set through sgc_set_tuning("linear_ck").
+int g_linear_ck = 64;
 
 // One LDS image per block (two barriers per chunk, half the LDS: twice the
 // blocks per CU) measured faster than the double buffer at the Reddit-train
@@ -281,7 +311,7 @@ hipError_t dispatch_nt(int nt, const float *X, int64_t ldx, const float *W, cons
 
 }  // namespace
 
-template <int V, int NT, int DIAG = 0>
+template <int V, int NT, int DIAG = 0, int CK = 32>
 hipError_t launch_stream(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                          int64_t ldy, int M, int K, int C, int Kp, size_t lds, hipStream_t s) {
     static int cus = 0;
@@ -294,7 +324,7 @@ hipError_t launch_stream(const float *X, int64_t ldx, const float *W, const floa
     }
     if (!attr[NT]) {
         hipError_t e = hipFuncSetAttribute(
-            reinterpret_cast<const void *>(&linear_stream_kernel<V, NT, DIAG>),
+            reinterpret_cast<const void *>(&linear_stream_kernel<V, NT, DIAG, CK>),
             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr[NT] = true;
@@ -302,7 +332,7 @@ hipError_t launch_stream(const float *X, int64_t ldx, const float *W, const floa
     // one workgroup per CU, at most one per tile
     const int tiles = (M + 15) / 16;
     const int blocks = std::max(1, std::min(cus, tiles));
-    hipLaunchKernelGGL((linear_stream_kernel<V, NT, DIAG>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((linear_stream_kernel<V, NT, DIAG, CK>), dim3((unsigned)blocks),
                        dim3(64 * kStreamWaves), lds, s, X, ldx, W, b, Y, ldy, M, K, C, Kp);
     return hipGetLastError();
 }
@@ -349,12 +379,17 @@ int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *
             const int Kp = (int)((K + 31) / 32 * 32);
             const bool v4 = ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0;
             hipError_t e;
-#define SGC_STREAM(VV)                                                                         \
-    switch (nt) {                                                                              \
-        case 1: e = launch_stream<VV, 1>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream); break; \
-        case 2: e = launch_stream<VV, 2>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream); break; \
-        case 3: e = launch_stream<VV, 3>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream); break; \
-        default: e = launch_stream<VV, 4>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream); break; \
+            const int Kp64 = (int)((K + 63) / 64 * 64);
+#define SGC_STREAM_NT(VV, NTV)                                                                  \
+    (g_linear_ck == 64                                                                          \
+         ? launch_stream<VV, NTV, 0, 64>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp64, lds, stream) \
+         : launch_stream<VV, NTV, 0, 32>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, Kp, lds, stream))
+#define SGC_STREAM(VV)                                  \
+    switch (nt) {                                       \
+        case 1: e = SGC_STREAM_NT(VV, 1); break;        \
+        case 2: e = SGC_STREAM_NT(VV, 2); break;        \
+        case 3: e = SGC_STREAM_NT(VV, 3); break;        \
+        default: e = SGC_STREAM_NT(VV, 4); break;       \
     }
             if (v4) {
                 SGC_STREAM(4)
@@ -362,6 +397,7 @@ int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *
                 SGC_STREAM(2)
             }
 #undef SGC_STREAM
+#undef SGC_STREAM_NT
             SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear launch failed: %s", hipGetErrorString(e));
             continue;
         }

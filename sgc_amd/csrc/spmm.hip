@@ -1668,6 +1668,11 @@ int set_tuning(const char *key, int64_t value) {
         g_tile_buffers = (int)value;
         return SGC_OK;
     }
+    if (std::string(key) == "linear_ck") {
+        SGC_REQUIRE(value == 32 || value == 64, SGC_EINVAL, "linear_ck must be 32 or 64");
+        g_linear_ck = (int)value;
+        return SGC_OK;
+    }
     if (std::string(key) == "linear_kernel") {
         SGC_REQUIRE(value >= 0 && value <= 4, SGC_EINVAL, "linear_kernel must be 0..4");
         g_linear_kernel = (int)value;
@@ -1693,6 +1698,7 @@ int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "hub_fuse") return g_hub_fuse;
     if (key && std::string(key) == "tile_buffers") return g_tile_buffers;
     if (key && std::string(key) == "linear_kernel") return g_linear_kernel;
+    if (key && std::string(key) == "linear_ck") return g_linear_ck;
     return -1;
 }
 

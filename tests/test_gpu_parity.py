@@ -573,8 +573,10 @@ def test_linear_tile_edges(tile_buffers, M, K, C, ld_extra):
 @pytest.mark.parametrize("M,K,C,ld_extra", [(129, 602, 41, 6), (300, 33, 17, 1), (257, 31, 3, 1),
                                             (128, 64, 64, 32), (1, 1, 1, 1), (500, 576, 70, 2),
                                             (70000, 602, 41, 0), (66000, 100, 48, 4)])
-def test_linear_stream_edges(M, K, C, ld_extra):
-    """The streaming forward (linear_stream_kernel, forced): W^T in LDS, X
+@pytest.mark.parametrize("ck", [32, 64])
+def test_linear_stream_edges(M, K, C, ld_extra, ck):
+    """The streaming forward (linear_stream_kernel, forced; 32- or 64-k
+    chunks): W^T in LDS, X
     streamed per 16-row tile with b128 (ld % 4 == 0) or b64 loads (ld = 602,
     the Reddit-train layout); rows past M read zeros, the last chunk's k >= K
     are zeroed (X holds infinities there); M = 70,000 / 66,000 give waves
@@ -589,7 +591,9 @@ def test_linear_stream_edges(M, K, C, ld_extra):
     b = torch.randn(C, generator=g)
     ref = torch.nn.functional.linear(Xf[:, :K].double(), W.double(), b.double())
     tol = 1e-5 * max(1.0, ref.abs().max().item())
+    prev_ck = lib.sgc_get_tuning(b"linear_ck")
     _lib.check(lib.sgc_set_tuning(b"linear_kernel", 2), "set_tuning")
+    _lib.check(lib.sgc_set_tuning(b"linear_ck", ck), "set_tuning")
     try:
         Xd = Xf.to(DEV)[:, :K]
         Y = linear(Xd, W.to(DEV), b.to(DEV)).cpu().double()
@@ -598,6 +602,7 @@ def test_linear_stream_edges(M, K, C, ld_extra):
         torch.testing.assert_close(Yn, ref - b.double(), rtol=1e-5, atol=tol)
     finally:
         lib.sgc_set_tuning(b"linear_kernel", 0)
+        lib.sgc_set_tuning(b"linear_ck", prev_ck)
 
 
 def test_sgc_model_autograd_matches_torch():
