@@ -316,17 +316,36 @@ int sgc_propagate_groups_f32(int32_t groups, const int32_t *row_ptrs, const int3
 int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd,
                      int64_t n_rows, int64_t F, void *stream);
 
+/* Batched 2-D block copy, one launch (the multi-GPU exchanges' unpack,
+ * sgc_amd.distributed): for each of nseg <= 64 segments, segs_host[6s ..
+ * 6s+5] = (src_row, src_col, dst_row, dst_col, rows, cols):
+ *     dst[dst_row + i, dst_col + j] = src[src_row + i, src_col + j],
+ * i < rows, j < cols; row strides lds / ldd (floats).  Segments must not
+ * overlap in dst.  Replaces the P strided copies that landed each rank's
+ * column block of an all-gathered row chunk in X_K (the reference returns the
+ * whole X_K from utils.py:92-97, so every rank needs all of it). */
+int sgc_copy_blocks_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int32_t nseg,
+                        const int64_t *segs_host, void *stream);
+
 /* The row stride (floats) the engine uses for its own feature buffers. */
 int64_t sgc_aligned_ld(int64_t F);
 
 /* ---------------------------------------------------------------------------
  * Classifier forward Y[M,C] = X[M,K] . W[C,K]^T + b[C]  (models.py:17-18,
- * nn.Linear) on fp32 MFMA (v_mfma_f32_16x16x4_f32).  b may be NULL.
- * X row stride ldx, Y row stride ldy.  Tolerance-equal to torch (summation
- * order differs), not bit-equal.
+ * nn.Linear) at fp32 precision on MFMA: where W's three bf16 images fit LDS
+ * (e.g. K = 602, C <= 42) and M >= 4096, every operand is split exactly into
+ * three bf16 pieces and the six products that reach fp32 precision run on
+ * v_mfma_f32_16x16x32_bf16; otherwise fp32 MFMA (v_mfma_f32_16x16x4_f32).
+ * b may be NULL.  X row stride ldx, Y row stride ldy.  Tolerance-equal to
+ * torch (summation order differs), not bit-equal.
  * ------------------------------------------------------------------------- */
 int sgc_linear_f32(const float *X, int64_t ldx, const float *W, const float *b,
                    float *Y, int64_t ldy, int64_t M, int64_t K, int64_t C, void *stream);
+
+/* Name of the kernel sgc_linear_f32 launches for these arguments (under the
+ * current "linear_kernel" tuning), for benchmark labels; "none" for an empty
+ * or invalid shape.  Static storage. */
+const char *sgc_linear_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C, const float *X);
 
 /* Backward of sgc_linear_f32 for the weights (what autograd runs for
  * nn.Linear after F.cross_entropy(model(x), y).backward() in the closures of
@@ -467,7 +486,7 @@ int sgc_mgpu_finalize(void);
  * `stream` (the current device) and waits for them, so those loads happen
  * here rather than inside the first sgc_precompute the caller times
  * (reddit.py:43,72-74).  Units: SGC_WARM_PROPAGATE = SpMM, ingest, plan,
- * sort, column groups; SGC_WARM_CLASSIFIER = linear, fused loss;
+ * sort, column groups, the exchanges' block copy; SGC_WARM_CLASSIFIER = linear, fused loss;
  * SGC_WARM_LOADERS = normalisation, sub-graph.  Synchronous. */
 enum { SGC_WARM_PROPAGATE = 1, SGC_WARM_CLASSIFIER = 2, SGC_WARM_LOADERS = 4 };
 int sgc_warmup(uint32_t units, void *stream);

@@ -52,8 +52,10 @@ SIGNATURES = {
     "sgc_propagate_groups_f32": (ctypes.c_int, [_i32, _p, _p, _p, _i64, _p, _i64, _p, _i64, _i64,
                                                  _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "sgc_pad_rows_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i64, _p]),
+    "sgc_copy_blocks_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i32, _p, _p]),
     "sgc_aligned_ld": (_i64, [_i64]),
     "sgc_linear_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
+    "sgc_linear_kernel_name": (ctypes.c_char_p, [_i64, _i64, _i64, _i64, _p]),
     "sgc_linear_xent_workspace": (_i64, [_i64, _i64, _i64]),
     "sgc_linear_xent_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _p, _p, _p,
                                            _p, _i64, _p, _i64, _p]),

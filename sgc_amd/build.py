@@ -13,7 +13,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsgc_amd.so")
 SOURCES = ["capi.hip", "spmm.hip", "ingest.hip", "linear.hip", "normalize.hip", "xent.hip",
-           "subgraph.hip", "cpu.hip", "mgpu.hip", "plan.hip", "groups.hip", "sort.hip"]
+           "subgraph.hip", "cpu.hip", "mgpu.hip", "plan.hip", "groups.hip", "sort.hip",
+           "exchange.hip"]
 
 
 def _headers():

@@ -88,7 +88,10 @@ def classifier_record(dev, M=152410, K=602, C=41, reps=20, epochs=2, seed=0):
     fwd_bytes = 4 * M * K + 4 * M * C + 4 * C * K
     bwd_bytes = 4 * M * K + 4 * M * C
     t = _median_ms(lambda: linear(x, W, b), reps)
-    rec["forward"] = {"kernel": "linear_kernel (sgc_linear_f32, v_mfma_f32_16x16x4f32)", "ms": t,
+    from . import _lib
+    kname = _lib.load().sgc_linear_kernel_name(M, K, x.stride(0), C, _lib.ptr(x)).decode()
+    rec["forward"] = {"kernel": f"{kname} (sgc_linear_f32; name from sgc_linear_kernel_name)",
+                      "ms": t,
                       "bytes": fwd_bytes, "achieved_GBps": fwd_bytes / t / 1e6,
                       "frac": fwd_bytes / t / 1e6 / HBM_PEAK_GBS,
                       "torch_F_linear_ms": _median_ms(lambda: F.linear(x, W, b), reps)}

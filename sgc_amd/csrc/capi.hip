@@ -34,6 +34,8 @@ int launch_spmm(const int32_t *row_ptr, const int32_t *col_idx, const float *val
                 int64_t n_hub, int32_t heavy_threshold, uint32_t flags, hipStream_t stream);
 int launch_pad_rows(const float *src, int64_t lds, float *dst, int64_t ldd, int64_t n_rows,
                     int64_t F, hipStream_t stream);
+int launch_copy_blocks(const float *src, int64_t lds, float *dst, int64_t ldd, int32_t nseg,
+                       const int64_t *segs, hipStream_t stream);
 size_t augnorm_scan_temp_bytes(int64_t n);
 int augnorm_count(const int32_t *row_ptr, const int32_t *col, const double *val, int64_t n,
                   int64_t nnz, int32_t *out_row_ptr, double *rowsum, void *ws, size_t ws_bytes,
@@ -75,6 +77,7 @@ int64_t propagate_cpu_workspace(int64_t n_rows, int64_t F, int32_t K);
 int propagate_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *val,
                   int64_t n_rows, const float *X0, int64_t ldx, float *out, int64_t ldo, int64_t F,
                   int32_t K, void *workspace, int64_t workspace_bytes, int32_t n_threads);
+const char *linear_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C, const float *X);
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                       int64_t ldy, int64_t M, int64_t K, int64_t C, hipStream_t stream);
 int64_t plan_sorted_workspace(int64_t n_rows);
@@ -236,6 +239,11 @@ int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int
     return launch_pad_rows(src, lds, dst, ldd, n_rows, F, as_stream(stream));
 }
 
+int sgc_copy_blocks_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int32_t nseg,
+                        const int64_t *segs_host, void *stream) {
+    return launch_copy_blocks(src, lds, dst, ldd, nseg, segs_host, as_stream(stream));
+}
+
 int sgc_propagate_groups_f32(int32_t groups, const int32_t *row_ptrs, const int32_t *col_idx,
                              const float *val, int64_t n_rows, const float *X0, int64_t ldx,
                              float *out, int64_t ldo, int64_t F, int32_t K,
@@ -319,6 +327,10 @@ int sgc_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, 
     return launch_linear_f32(X, ldx, W, b, Y, ldy, M, K, C, as_stream(stream));
 }
 
+const char *sgc_linear_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C, const float *X) {
+    return linear_kernel_name(M, K, ldx, C, X);
+}
+
 int64_t sgc_linear_backward_workspace(int64_t M, int64_t K, int64_t C) {
     return linear_backward_workspace_bytes(M, K, C);
 }
@@ -351,6 +363,7 @@ int sgc_warmup(uint32_t units, void *stream) {
         SGC_HIP_CHECK(warm_plan(s));
         SGC_HIP_CHECK(warm_sort(s));
         SGC_HIP_CHECK(warm_groups(s));
+        SGC_HIP_CHECK(warm_exchange(s));
     }
     if (units & SGC_WARM_CLASSIFIER) {
         SGC_HIP_CHECK(warm_linear(s));

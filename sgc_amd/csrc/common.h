@@ -48,6 +48,7 @@ hipError_t warm_ingest(hipStream_t);
 hipError_t warm_plan(hipStream_t);
 hipError_t warm_sort(hipStream_t);
 hipError_t warm_groups(hipStream_t);
+hipError_t warm_exchange(hipStream_t);
 hipError_t warm_linear(hipStream_t);
 hipError_t warm_xent(hipStream_t);
 hipError_t warm_normalize(hipStream_t);

@@ -10,6 +10,11 @@
 // once from HBM in whole lines and W once per block from L2.  At the Reddit-train
 // shape the fp32 MFMA work (2 x 152,410 x 602 x 48 = 8.8 GFLOP, 56 us at
 // 157 TF) and the X read (367 MB, ~60 us) are about even.
+#include <map>
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "gemm_tile.h"
 
 namespace sgc {
@@ -267,9 +272,244 @@ __global__ __launch_bounds__(64 * kStreamWaves) void linear_stream_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Split-bf16 streaming form (round 5, the default where its W image fits LDS).
+// The fp32 MFMA runs at 1/16 of the bf16 rate, and at the Reddit-train shape
+// its 4.34 M MFMAs alone (56 us at peak) are as long as the X stream: the
+// round-4 kernel could not overlap the two.  Here every fp32 operand is split
+// into three bf16 pieces, x = h + m + l EXACTLY (h = RNE(x), m = RNE(x - h),
+// l = x - h - m; each difference is exact by Sterbenz), and x . w is taken as
+// the six products that reach fp32 precision -- hh, hm, mh, hl, lh, mm (the
+// dropped ml, lm, ll are below 2^-25 of |x||w|) -- on v_mfma_f32_16x16x32_bf16,
+// whose bf16 x bf16 products are exact in its fp32 sums: 6/16 of the fp32 MFMA
+// time, so the X stream alone sets the pace.  Tolerance parity with fp32
+// (test_linear_split_*); X values past +-3.39e38 (bf16's largest finite) are
+// not supported.
+// * X stream: per 32-k chunk of a 16-row tile a lane issues two b128 loads,
+//   each wave-instruction reading 128 contiguous bytes of each of 8 rows (8
+//   lanes per row): instruction 0 rows 0-7, instruction 1 rows 8-15, lane
+//   (j, kg) = (l & 15, l >> 4) at byte 16 * (2 kg + (j >> 3)) of the chunk.
+//   The round-4 shape (64 B of each of 16 rows, the MFMA operand layout
+//   loaded directly) streamed at 2.4-3.2 TB/s, this one at 5.5-5.8
+//   (scripts/micro/stream_shape.hip, profiles/r05/stream_shape.log).  One DPP
+//   row_ror:8 exchange per register then gives lane (j, kg) floats 8kg..8kg+7
+//   of row j -- the bf16 16x16x32 A operand, k in natural order.
+// * W's three bf16 images (C rows each, not padded to the class tile; rows
+//   past C read as zeros) stay in LDS for the whole persistent launch, 16-B
+//   granules XOR-swizzled per 128-k window (conflict-free ds_read_b128).
+// * Two accumulator sets per class tile, the hh products and the five small
+//   ones, summed at the store.
+constexpr int kSplitDepth = 4;  // chunks in flight per wave
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// 0 = auto (streaming where W fits LDS and the rows are 8-B aligned), 1 = the
-// LDS tile, 2 = streaming (3 / 4: its DIAG forms, wrong results by design).
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+    const bf16x2_t v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32 (RNE)
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+// (a, b) -> packed hi / mid / lo bf16 pairs with a == hi + mid + lo exactly.
+// A non-finite residual (x infinite) is taken as 0, so x = +-inf keeps its
+// hi . w products as the fp32 sum would.
+__device__ __forceinline__ void split3(float a, float b, uint32_t &h, uint32_t &m, uint32_t &l) {
+    h = pk_bf16(a, b);
+    float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+    ra = __builtin_fabsf(ra) <= 3.402823466e38f ? ra : 0.0f;
+    rb = __builtin_fabsf(rb) <= 3.402823466e38f ? rb : 0.0f;
+    m = pk_bf16(ra, rb);
+    l = pk_bf16(ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u));
+}
+
+__device__ __forceinline__ float ror8(float x) {  // lane j of each 16-lane row gets lane j ^ 8's x
+    return __builtin_bit_cast(
+        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128, 0xf, 0xf, false));
+}
+
+// DIAG 1: the loads and the exchange only (the X stream's own time).
+template <int NT, int NW, int DIAG = 0>
+__global__ __launch_bounds__(64 * NW) void linear_split_kernel(
+    const float *__restrict__ X, int64_t ldx, const float *__restrict__ W,
+    const float *__restrict__ b, float *__restrict__ Y, int64_t ldy, int M, int K, int C, int S) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    // image p (0 hi, 1 mid, 2 lo), row r < C: granules [(p * C + r) * S, + S);
+    // granule q (k = 8q .. 8q + 7) of row r at (q & ~15) | ((q ^ r) & 15)
+    extern __shared__ __attribute__((aligned(16))) u32x4 sgr[];
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, kg = lane >> 4;
+    for (int base = threadIdx.x; base < C * S; base += 4 * 64 * NW) {
+        float v[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = base + u * 64 * NW;
+            const int r = idx / S, q = idx - r * S;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int k = 8 * q + e;
+                v[u][e] = (idx < C * S && k < K) ? W[(int64_t)r * K + k] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = base + u * 64 * NW;
+            if (idx >= C * S) break;
+            const int r = idx / S, q = idx - r * S;
+            uint32_t h[4], m[4], l[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) split3(v[u][2 * p], v[u][2 * p + 1], h[p], m[p], l[p]);
+            const int slot = (q & ~15) | ((q ^ r) & 15);
+            sgr[(0 * C + r) * S + slot] = u32x4{h[0], h[1], h[2], h[3]};
+            sgr[(1 * C + r) * S + slot] = u32x4{m[0], m[1], m[2], m[3]};
+            sgr[(2 * C + r) * S + slot] = u32x4{l[0], l[1], l[2], l[3]};
+        }
+    }
+    int *next = reinterpret_cast<int *>(sgr + 3 * C * S);
+    if (threadIdx.x == 0) *next = 0;
+    __syncthreads();
+    const int n_tiles = (M + 15) >> 4;
+    auto grab = [&]() -> int {  // the workgroup's next tile (block + grid * m), or -1
+        int m = 0;
+        if (lane == 0) m = atomicAdd(next, 1);
+        m = __builtin_amdgcn_readfirstlane(m);
+        const int t = (int)blockIdx.x + (int)gridDim.x * m;
+        return t < n_tiles ? t : -1;
+    };
+    const int NC = (K + 31) / 32;  // chunks per tile
+    const auto xd = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(X), 0, (int)((int64_t)M * ldx * 4), 0x00020000);  // < 2^31
+    const uint32_t seg = 16u * (2 * kg + (j >> 3));
+    const uint32_t pitch8 = (uint32_t)(8 * ldx * 4);
+    int ltile = grab(), lc = 0;
+    uint32_t lrow0 = 0, lrow1 = 0;
+    auto rows_of = [&](int tile) {
+        const int row = tile * 16 + (j & 7);
+        lrow0 = (tile >= 0 && row < M) ? (uint32_t)((int64_t)row * ldx * 4) + seg : kOffOOB;
+        lrow1 = (tile >= 0 && row + 8 < M) ? lrow0 + pitch8 : kOffOOB;
+    };
+    rows_of(ltile);
+    constexpr int D = kSplitDepth;
+    f4 xa[D], xb[D];
+    int stile[D], sc[D];
+    // Both loads are issued on every path (past the last tile their offsets
+    // are out of range: zeros, no memory traffic), so every path has the same
+    // loads in flight and the compiler's counted waits stay vmcnt(2 (D - 1))
+    // instead of draining the ring (vmcnt(0)) at each chunk.
+    auto load = [&](int slot) {
+        stile[slot] = ltile;
+        sc[slot] = lc;
+        const uint32_t co = (uint32_t)lc * 128u;
+        xa[slot] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xd, lrow0 + co, 0, 0));
+        xb[slot] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xd, lrow1 + co, 0, 0));
+        if (ltile >= 0 && ++lc == NC) {
+            lc = 0;
+            ltile = grab();
+            rows_of(ltile);
+        }
+    };
+    // the bias of the lane's classes, read before the stream starts (a global
+    // load in the loop would make the tile's stores wait for every X load)
+    float bias[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) bias[n] = (b && n * 16 + j < C) ? b[n * 16 + j] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < D; ++u) load(u);
+    f32x4 accH[NT], accL[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) accH[n] = accL[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool low = j < 8;
+    for (;;) {
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+            const int tile = stile[u], c = sc[u];
+            if (tile < 0) return;  // wave-uniform: the stream is in order
+            // W operands of chunk c: granule 4c + kg of row n * 16 + j of each image
+            u32x4 bw[NT][3];
+            {
+                const int q = 4 * c + kg;
+                const int slot = (q & ~15) | ((q ^ j) & 15);
+#pragma unroll
+                for (int n = 0; n < NT; ++n) {
+                    const int r = n * 16 + j;
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        bw[n][p] = (r < C) ? sgr[(p * C + r) * S + slot] : u32x4{0u, 0u, 0u, 0u};
+                }
+            }
+            const f4 A = xa[u], B = xb[u];
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float t = ror8(low ? B[e] : A[e]);
+                v[e] = low ? A[e] : t;
+                v[4 + e] = low ? t : B[e];
+            }
+            load(u);  // the chunk D ahead into the slot just consumed
+            if ((c + 1) * 32 > K) {  // the ragged last chunk (uniform)
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    if (c * 32 + 8 * kg + e >= K) v[e] = 0.0f;
+            }
+            if constexpr (DIAG == 1 || DIAG == 2) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) accH[0][e & 3] += v[e];
+            } else {
+                uint32_t ah[4], am[4], al[4];
+#pragma unroll
+                for (int p = 0; p < 4; ++p) split3(v[2 * p], v[2 * p + 1], ah[p], am[p], al[p]);
+                const bf16x8_t Ah = __builtin_bit_cast(bf16x8_t, u32x4{ah[0], ah[1], ah[2], ah[3]});
+                const bf16x8_t Am = __builtin_bit_cast(bf16x8_t, u32x4{am[0], am[1], am[2], am[3]});
+                const bf16x8_t Al = __builtin_bit_cast(bf16x8_t, u32x4{al[0], al[1], al[2], al[3]});
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    accH[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        Ah, __builtin_bit_cast(bf16x8_t, bw[n][0]), accH[n], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        Ah, __builtin_bit_cast(bf16x8_t, bw[n][1]), accL[n], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        Am, __builtin_bit_cast(bf16x8_t, bw[n][0]), accL[n], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        Ah, __builtin_bit_cast(bf16x8_t, bw[n][2]), accL[n], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        Al, __builtin_bit_cast(bf16x8_t, bw[n][0]), accL[n], 0, 0, 0);
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+                    accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        Am, __builtin_bit_cast(bf16x8_t, bw[n][1]), accL[n], 0, 0, 0);
+            }
+            if (DIAG >= 2 && c == NC - 1) {  // diagnostics without the Y stores
+                if (accH[0][0] == 12345.0f) Y[lane] = accH[0][1];
+                continue;
+            }
+            if (c == NC - 1) {  // tile done: D[4 kg + r][j] = row 4 kg + r, class n * 16 + j
+                const int m0 = tile * 16 + 4 * kg;
+#pragma unroll
+                for (int n = 0; n < NT; ++n) {
+                    const int cl = n * 16 + j;
+                    if (cl < C) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (m0 + r < M)
+                                Y[(int64_t)(m0 + r) * ldy + cl] = accH[n][r] + accL[n][r] + bias[n];
+                    }
+                    accH[n] = accL[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+        }
+    }
+}
+
+// 0 = auto (split-bf16 streaming where W's images fit LDS, else fp32
+// streaming where W^T fits and the rows are 8-B aligned, else the LDS tile),
+// 1 = the LDS tile, 2 = fp32 streaming (3 / 4: its DIAG forms, wrong results
+// by design), 5 = split-bf16 streaming (6: its loads-only DIAG form).
 // Set through sgc_set_tuning("linear_kernel").
 int g_linear_kernel = 0;
 // k per chunk of the streaming kernel, 32 or 64 (64: forward 0.1237-0.1238
@@ -311,29 +551,71 @@ hipError_t dispatch_nt(int nt, const float *X, int64_t ldx, const float *W, cons
 
 }  // namespace
 
+// The current device's CU count, and the 160 KB dynamic-LDS attribute of a
+// persistent kernel raised once per (device, kernel): both kept per device
+// under a lock (a process may launch on several devices, from several threads).
+hipError_t persistent_setup(const void *kernel, int *cus) {
+    static std::mutex mu;
+    static std::map<int, int> cu_count;
+    static std::set<std::pair<int, const void *>> raised;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cu_count.find(dev);
+    if (it == cu_count.end()) {
+        int n = 0;
+        e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        it = cu_count.emplace(dev, n).first;
+    }
+    *cus = it->second;
+    if (!raised.count({dev, kernel})) {
+        e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        raised.insert({dev, kernel});
+    }
+    return hipSuccess;
+}
+
 template <int V, int NT, int DIAG = 0, int CK = 32>
 hipError_t launch_stream(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                          int64_t ldy, int M, int K, int C, int Kp, size_t lds, hipStream_t s) {
-    static int cus = 0;
-    static bool attr[5] = {false, false, false, false, false};
-    if (!cus) {
-        int dev = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e != hipSuccess) return e;
-    }
-    if (!attr[NT]) {
-        hipError_t e = hipFuncSetAttribute(
-            reinterpret_cast<const void *>(&linear_stream_kernel<V, NT, DIAG, CK>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr[NT] = true;
-    }
+    int cus = 0;
+    hipError_t e = persistent_setup(
+        reinterpret_cast<const void *>(&linear_stream_kernel<V, NT, DIAG, CK>), &cus);
+    if (e != hipSuccess) return e;
     // one workgroup per CU, at most one per tile
     const int tiles = (M + 15) / 16;
     const int blocks = std::max(1, std::min(cus, tiles));
     hipLaunchKernelGGL((linear_stream_kernel<V, NT, DIAG, CK>), dim3((unsigned)blocks),
                        dim3(64 * kStreamWaves), lds, s, X, ldx, W, b, Y, ldy, M, K, C, Kp);
+    return hipGetLastError();
+}
+
+constexpr int kSplitWaves = 8;
+
+// Split-bf16 kernel: W's three images, C rows of S granules each, + the tile
+// counter; S covers the chunks' k rounded up to a 128-k swizzle window.
+inline int split_granules(int64_t K) { return (int)(((K + 31) / 32 * 4 + 15) / 16 * 16); }
+inline size_t split_lds(int64_t K, int C) { return (size_t)3 * C * split_granules(K) * 16 + 16; }
+
+bool split_fits(int64_t M, int64_t K, int64_t ldx, int C) {
+    return split_lds(K, C) <= 160 * 1024 && M * ldx * 4 < INT32_MAX && K < (int64_t(1) << 24);
+}
+
+template <int NT, int DIAG>
+hipError_t launch_split(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
+                        int64_t ldy, int M, int K, int C, hipStream_t s) {
+    int cus = 0;
+    hipError_t e = persistent_setup(
+        reinterpret_cast<const void *>(&linear_split_kernel<NT, kSplitWaves, DIAG>), &cus);
+    if (e != hipSuccess) return e;
+    const int tiles = (M + 15) / 16;
+    const int blocks = std::max(1, std::min(cus, tiles));
+    hipLaunchKernelGGL((linear_split_kernel<NT, kSplitWaves, DIAG>), dim3((unsigned)blocks),
+                       dim3(64 * kSplitWaves), split_lds(K, C), s, X, ldx, W, b, Y, ldy, M, K, C,
+                       split_granules(K));
     return hipGetLastError();
 }
 
@@ -343,6 +625,27 @@ bool stream_fits(int64_t M, int64_t K, int64_t ldx, int nt, const float *X, size
     *lds = (size_t)nt * 16 * ((K + 63) / 64 * 64) * 4 + 16;  // + the tile counter
     return *lds <= 160 * 1024 && M * ldx * 4 < INT32_MAX && ldx % 2 == 0 &&
            reinterpret_cast<uintptr_t>(X) % 8 == 0;
+}
+
+// Which forward kernel a class block of cc <= 64 classes takes (the
+// diagnostic forms, tuning 3 / 4 / 6, count as their kernel).
+enum LinearChoice { kLinTile, kLinStream, kLinSplit };
+LinearChoice linear_choice(int64_t M, int64_t K, int64_t ldx, int cc, const float *X) {
+    size_t lds = 0;
+    const bool stream_ok = stream_fits(M, K, ldx, (cc + 15) / 16, X, &lds);
+    const bool split_ok = split_fits(M, K, ldx, cc);
+    if (g_linear_kernel >= 5 || (g_linear_kernel == 0 && split_ok && M >= 4096)) return kLinSplit;
+    if (g_linear_kernel >= 2 || (g_linear_kernel == 0 && stream_ok && M >= 4096)) return kLinStream;
+    return kLinTile;
+}
+
+const char *linear_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C, const float *X) {
+    static const char *names[] = {
+        "linear_kernel (LDS tile, v_mfma_f32_16x16x4_f32)",
+        "linear_stream_kernel (fp32 streaming, v_mfma_f32_16x16x4_f32)",
+        "linear_split_kernel (split-bf16 streaming, v_mfma_f32_16x16x32_bf16 x 6 products)"};
+    if (M <= 0 || K <= 0 || C <= 0 || ldx < K) return "none";
+    return names[linear_choice(M, K, ldx, (int)std::min<int64_t>(C, 64), X)];
 }
 
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
@@ -365,6 +668,26 @@ int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *
         float *Yc = Y + c0;
         size_t lds = 0;
         const bool stream_ok = stream_fits(M, K, ldx, nt, X, &lds);
+        const bool split_ok = split_fits(M, K, ldx, cc);
+        if (linear_choice(M, K, ldx, cc, X) == kLinSplit) {
+            SGC_REQUIRE(split_ok, SGC_EINVAL, "linear: split kernel preconditions not met");
+            hipError_t e;
+            const int diag = g_linear_kernel - 5;
+#define SGC_SPLIT_NT(NTV)                                                                       \
+    (diag == 1 ? launch_split<NTV, 1>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, stream)    \
+     : diag == 2 ? launch_split<NTV, 2>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, stream)  \
+     : diag == 3 ? launch_split<NTV, 3>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, stream)  \
+                 : launch_split<NTV, 0>(X, ldx, Wc, bc, Yc, ldy, (int)M, (int)K, cc, stream))
+            switch (nt) {
+                case 1: e = SGC_SPLIT_NT(1); break;
+                case 2: e = SGC_SPLIT_NT(2); break;
+                case 3: e = SGC_SPLIT_NT(3); break;
+                default: e = SGC_SPLIT_NT(4); break;
+            }
+#undef SGC_SPLIT_NT
+            SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear launch failed: %s", hipGetErrorString(e));
+            continue;
+        }
         if (g_linear_kernel >= 3) {  // diagnostics: NT = 3, 8-B rows only
             SGC_REQUIRE(stream_ok && nt == 3, SGC_EINVAL, "linear: diagnostic kernel needs NT = 3");
             const int Kp = (int)((K + 31) / 32 * 32);
@@ -374,7 +697,7 @@ int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *
             SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear launch failed: %s", hipGetErrorString(e));
             continue;
         }
-        if (g_linear_kernel == 2 || (g_linear_kernel == 0 && stream_ok && M >= 4096)) {
+        if (linear_choice(M, K, ldx, cc, X) == kLinStream) {
             SGC_REQUIRE(stream_ok, SGC_EINVAL, "linear: streaming kernel preconditions not met");
             const int Kp = (int)((K + 31) / 32 * 32);
             const bool v4 = ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0;

@@ -1674,7 +1674,7 @@ int set_tuning(const char *key, int64_t value) {
         return SGC_OK;
     }
     if (std::string(key) == "linear_kernel") {
-        SGC_REQUIRE(value >= 0 && value <= 4, SGC_EINVAL, "linear_kernel must be 0..4");
+        SGC_REQUIRE(value >= 0 && value <= 8, SGC_EINVAL, "linear_kernel must be 0..8");
         g_linear_kernel = (int)value;
         return SGC_OK;
     }

@@ -1053,10 +1053,8 @@ class TiledPropagator:
         if out is None:
             out = torch.empty((rows, F), dtype=torch.float32, device=X0.device)
         R1 = max(1, rows)
-        for q in range(self.C):
-            q0, q1 = int(fb[q]), int(fb[q + 1])
-            if q1 > q0 and rows:
-                _copy_cols(full[q * R1:q * R1 + rows, :q1 - q0], out[:, q0:q1])
+        _copy_blocks(full, out, [(q * R1, 0, 0, int(fb[q]), rows, int(fb[q + 1] - fb[q]))
+                                 for q in range(self.C)])
         return out
 
 
@@ -1093,6 +1091,38 @@ def _copy_cols(src, dst):
             dst.shape[1], _lib.stream_handle(src.device)), "pad_rows_f32")
     else:
         dst.copy_(src)
+
+
+def _copy_blocks(src, dst, segs):
+    """For (src_row, src_col, dst_row, dst_col, rows, cols) in segs:
+    dst[dst_row:+rows, dst_col:+cols] = src[src_row:+rows, src_col:+cols], for
+    2-D views with unit column stride: one sgc_copy_blocks_f32 launch per 64
+    segments on the GPU (the exchanges' unpack: every rank's block of a
+    gathered chunk at once), torch copies on the CPU."""
+    segs = [tuple(int(v) for v in sg) for sg in segs if sg[4] > 0 and sg[5] > 0]
+    if not segs:
+        return
+    if not src.is_cuda:
+        for sr, sc, dr, dc, r, c in segs:
+            dst[dr:dr + r, dc:dc + c].copy_(src[sr:sr + r, sc:sc + c])
+        return
+    import ctypes
+    from . import _lib
+    lib = _lib.load()
+    for i in range(0, len(segs), 64):
+        part = segs[i:i + 64]
+        arr = (ctypes.c_int64 * (6 * len(part)))(*[v for sg in part for v in sg])
+        _lib.check(lib.sgc_copy_blocks_f32(_lib.ptr(src), src.stride(0), _lib.ptr(dst),
+                                           dst.stride(0), len(part), arr,
+                                           _lib.stream_handle(src.device)), "copy_blocks_f32")
+
+
+def _gather_slot(full, p, rows):
+    """Rank p's slot of an all-gather buffer [P*rows, ld]: the last hop writes
+    its rows there and the gather runs in place (NCCL/RCCL in-place
+    all-gather: sendbuff = recvbuff + rank*count), so the rank's own block is
+    never copied."""
+    return full[p * rows:(p + 1) * rows]
 
 
 class FeaturePartitionedPropagator:
@@ -1161,6 +1191,12 @@ class FeaturePartitionedPropagator:
         self.exchange = exchange
         self.pieces = pieces
         self._bufs = {}
+
+    # test hook: run the exchange through the process group even at world 1
+    # (the one-rank shortcuts skip it), so a one-GPU box exercises the RCCL
+    # calls -- async all-gathers from a side stream, in-place slots, waits
+    # across streams -- that P > 1 runs
+    force_collectives = False
 
     def _buf(self, key, shape, like):
         b = self._bufs.get(key)
@@ -1245,10 +1281,8 @@ class FeaturePartitionedPropagator:
         for w_ in works:
             w_.wait()
         rows = mine1 - mine0
-        for s_ in range(P):
-            q0, q1 = int(bounds[s_]), int(bounds[s_ + 1])
-            if s_ != p and q1 > q0 and rows:
-                _copy_cols(recv[s_ * Bn:s_ * Bn + rows, :q1 - q0], out[:, q0:q1])
+        _copy_blocks(recv, out, [(s_ * Bn, 0, 0, int(bounds[s_]), rows,
+                                  int(bounds[s_ + 1] - bounds[s_])) for s_ in range(P) if s_ != p])
         return out
 
     def propagate(self, X0, K, out=None, output="replicated"):
@@ -1298,7 +1332,7 @@ class FeaturePartitionedPropagator:
             if w and n:
                 hop(src, 0, n, dst, own, True)
             src, own = dst, True
-        if P == 1:  # one rank: the last hop writes X_K itself, nothing to exchange
+        if P == 1 and not self.force_collectives:  # the last hop writes X_K itself
             if w and n:
                 hop(src, 0, n, out, own, False)
             return out
@@ -1319,28 +1353,28 @@ class FeaturePartitionedPropagator:
             if work is not None:
                 work.wait()
             rows = int(rb[p + 1] - rb[p])
-            for q in range(P):
-                q0, q1 = int(bounds[q]), int(bounds[q + 1])
-                if q1 > q0 and rows:
-                    _copy_cols(recv[q * Bn:q * Bn + rows, :q1 - q0], out[:, q0:q1])
+            _copy_blocks(recv, out, [(q * Bn, 0, 0, int(bounds[q]), rows,
+                                      int(bounds[q + 1] - bounds[q])) for q in range(P)])
             return out
-        # last hop in row chunks, each gathered as soon as it is computed
+        # last hop in row chunks, each computed into this rank's slot of the
+        # chunk's gather buffer and gathered in place as soon as it is done;
+        # every gathered chunk then lands in X_K's columns in one launch
         pending = []
         for ci, (r0, r1) in enumerate(row_chunks(n, self.chunks)):
             rows = r1 - r0
-            loc = self._buf(("loc", ci), (rows, B), X0)
-            if w and rows:
-                hop(src, r0, r1, loc[:, :w], own, True)
+            if not rows:
+                continue
             full = self._buf(("full", ci), (P * rows, B), X0)
-            pending.append((r0, r1, full, self._all_gather(full, loc) if rows else None))
+            loc = _gather_slot(full, p, rows)
+            if w:
+                hop(src, r0, r1, loc[:, :w], own, True)
+            pending.append((r0, r1, full, self._all_gather(full, loc)))
         for r0, r1, full, work in pending:
             if work is not None:
                 work.wait()  # the compute stream waits for this chunk's gather
             rows = r1 - r0
-            for q in range(P):
-                q0, q1 = int(bounds[q]), int(bounds[q + 1])
-                if q1 > q0 and rows:
-                    _copy_cols(full[q * rows:(q + 1) * rows, :q1 - q0], out[r0:r1, q0:q1])
+            _copy_blocks(full, out, [(q * rows, 0, r0, int(bounds[q]), rows,
+                                      int(bounds[q + 1] - bounds[q])) for q in range(P)])
         return out
 
 
@@ -1431,8 +1465,10 @@ class LinePartitionedPropagator:
             self._tail_stream = torch.cuda.Stream(device)
         return torch.cuda.stream(self._tail_stream)
 
+    force_collectives = False  # test hook, as FeaturePartitionedPropagator's
+
     def _collective(self, kind, dst, src):
-        if self.world_size == 1:
+        if self.world_size == 1 and not self.force_collectives:
             return _local_copy(dst, src)
         fn = dist.all_gather_into_tensor if kind == "gather" else dist.all_to_all_single
         if not self.host_staging:
@@ -1447,11 +1483,12 @@ class LinePartitionedPropagator:
         may span several ranks' blocks)."""
         sh = self.shard
         B = sh.block
+        segs = []
         for q in range(self.world_size):
             a, b = max(r0, int(sh.bounds[q])), min(r1, int(sh.bounds[q + 1]))
             if b > a:
-                s = q * B + a - int(sh.bounds[q])
-                _copy_cols(full[s:s + b - a, :wt], dst[a - r0:b - r0])
+                segs.append((q * B + a - int(sh.bounds[q]), 0, a - r0, 0, b - a, wt))
+        _copy_blocks(full, dst, segs)
 
     def propagate(self, X0, K, out=None, output="replicated"):
         if output not in ("replicated", "sharded"):
@@ -1513,10 +1550,13 @@ class LinePartitionedPropagator:
                 with self._tail_ctx(X0.device):
                     if work is not None:
                         work.wait()
-                    loc = self._buf(("tl", k & 1), (B, ldt), X0)
+                    # this hop's gather buffer (hop k-1's is the one being
+                    # read: two alternate); the tail launch writes our slot
+                    # and the gather runs in place
+                    full = self._buf(("tf", k & 1), (P * B, ldt), X0)
+                    loc = _gather_slot(full, p, B)
                     if sh.rows:
                         self.tail_spmm_fn(sh, tsrc, loc[:sh.rows, :tw], tlayout)
-                    full = self._buf(("tf", k & 1), (P * B, ldt), X0)
                     work = self._collective("gather", full, loc)
                     if work is None and gpu:  # staged: the copy is done on this stream
                         work = _StreamDone(torch.cuda.current_stream(X0.device))
@@ -1541,31 +1581,36 @@ class LinePartitionedPropagator:
 
     def _last_replicated(self, msrc, mown, out, main_hop, W, w, ld, P, X0):
         n, F = out.shape
-        if P == 1:
+        if P == 1 and not self.force_collectives:
             if w and n:
                 main_hop(msrc, 0, n, out[:, :w], mown, False)
             return
+        if W == 0:  # all-tail layout (F < 32 P): no main blocks to exchange (W is
+            return  # the same on every rank, so every rank skips the same calls)
+        p = self.rank
         pending = []
         for ci, (r0, r1) in enumerate(row_chunks(n, self.chunks)):
             rows = r1 - r0
-            loc = self._buf(("loc", ci), (rows, ld), X0)
-            if w and rows:
-                main_hop(msrc, r0, r1, loc[:, :w], mown, True)
+            if not rows:
+                continue
             full = self._buf(("full", ci), (P * rows, ld), X0)
-            pending.append((r0, r1, full, self._collective("gather", full, loc) if rows else None))
+            loc = _gather_slot(full, p, rows)  # in-place gather: no copy of our block
+            if w:
+                main_hop(msrc, r0, r1, loc[:, :w], mown, True)
+            pending.append((r0, r1, full, self._collective("gather", full, loc)))
         for r0, r1, full, work in pending:
             if work is not None:
                 work.wait()
             rows = r1 - r0
-            for q in range(P):
-                q0, q1 = min(q * W, F), min((q + 1) * W, F)
-                if q1 > q0 and rows:
-                    _copy_cols(full[q * rows:(q + 1) * rows, :q1 - q0], out[r0:r1, q0:q1])
+            _copy_blocks(full, out, [(q * rows, 0, r0, min(q * W, F), rows,
+                                      min((q + 1) * W, F) - min(q * W, F)) for q in range(P)])
 
     def _last_sharded(self, msrc, mown, out, main_hop, W, w, rb, P, X0):
         n = msrc.shape[0]
         F = out.shape[1]
         p = self.rank
+        if W == 0:  # all-tail layout: nothing in the main blocks (same on every rank)
+            return
         Bn = max(1, -(-n // P))
         ldw = max(W, 1)
         send = self._buf("send", (P * Bn, ldw), X0)
@@ -1576,10 +1621,8 @@ class LinePartitionedPropagator:
         if work is not None:
             work.wait()
         rows = int(rb[p + 1] - rb[p])
-        for q in range(P):
-            q0, q1 = min(q * W, F), min((q + 1) * W, F)
-            if q1 > q0 and rows:
-                _copy_cols(recv[q * Bn:q * Bn + rows, :q1 - q0], out[:, q0:q1])
+        _copy_blocks(recv, out, [(q * Bn, 0, 0, min(q * W, F), rows,
+                                  min((q + 1) * W, F) - min(q * W, F)) for q in range(P)])
 
 
 # ---------------------------------------------------------------------------

@@ -17,25 +17,35 @@ either of two ways:
   native multi-device engine of the C ABI (sgc_mgpu_*, csrc/mgpu.hip) drives
   all of them from the single call; see `DeviceSet`.
 
-Partition (SGC_AMD_PARTITION): "auto" (default) = "lines" from 4 ranks,
-"features" below; "features" -- each rank runs all K hops over the whole S on
+Partition (SGC_AMD_PARTITION): "auto" (default) -- chosen by measured time:
+the first call on an adjacency (per group, feature width and K) runs every
+candidate of AUTO_CANDIDATES once to warm it and once timed, takes the
+slowest rank's time of each (one all-reduce), keeps the fastest for every
+later call and returns its X_K (all candidates give the same bits), so the
+replicated call is never slower than one GPU's: "replicate" is a candidate;
+"replicate" -- every rank computes all of X_K itself (no exchange; one GPU's
+time at any P); "features" -- each rank runs all K hops over the whole S on
 its block of feature columns, so the only exchange is one all-gather of X_K,
-the least any replicated output can move; "lines" -- each rank owns whole
-128-B lines of features plus a row block of the leftover lines, gathered
-after each hop (per-rank compute at Reddit shape, one GPU per rank: P = 4
-2.44 vs 3.03 ms, P = 8 1.52 vs 1.62; P = 2 5.44 vs 5.19, DESIGN.md 6.3);
-"rows" (nnz-balanced row blocks, an all-gather of X_k per hop: the north
-star's 1-D row slicing) or "cyclic" (row tiles round-robin, column-ordered
-exchange).
+the least any partitioned replicated output can move; "lines" -- each rank
+owns whole 128-B lines of features plus a row block of the leftover lines,
+gathered after each hop (per-rank compute at Reddit shape, one GPU per rank:
+P = 4 2.44 vs 3.03 ms, P = 8 1.52 vs 1.62; P = 2 5.44 vs 5.19, DESIGN.md
+6.3); "rows" (nnz-balanced row blocks, an all-gather of X_k per hop: the
+north star's 1-D row slicing) or "cyclic" (row tiles round-robin,
+column-ordered exchange).
 Every partition keeps each output element's FMA chain whole and in CSR
 order, so X_K is bit-identical to one GPU's and to the reference.
 """
 import os
+import time
 
 import torch
 import torch.distributed as dist
 
-PARTITIONS = ("auto", "features", "lines", "rows", "cyclic")
+PARTITIONS = ("auto", "replicate", "features", "lines", "rows", "cyclic")
+# what "auto" times on the first call (the row and cyclic partitions move X_k
+# after every hop: never faster for a replicated X_K, DESIGN.md 6.4)
+AUTO_CANDIDATES = ("replicate", "features", "lines")
 
 
 def torchrun_env():
@@ -97,14 +107,12 @@ def process_group(device):
 
 
 def partition_name(world=None):
-    """The partition SGC_AMD_PARTITION names; "auto" (the default) resolves
-    to "lines" at world >= 4 and "features" below (returned as "auto" when
-    no world size is given)."""
+    """The partition SGC_AMD_PARTITION names ("auto", the default, is chosen
+    by measured time on the first call: precompute_group).  `world` is
+    accepted for the callers that pass it; it does not change the name."""
     p = os.environ.get("SGC_AMD_PARTITION", "auto")
     if p not in PARTITIONS:
         raise ValueError(f"SGC_AMD_PARTITION must be one of {PARTITIONS}, not {p!r}")
-    if p == "auto" and world is not None:
-        return "lines" if world >= 4 else "features"
     return p
 
 
@@ -127,7 +135,9 @@ def _propagator(csr, group, partition, staging):
     prop = csr._plans.get(key)
     if prop is not None:
         return prop
-    if partition == "features":
+    if partition == "replicate":
+        prop = ReplicatedPropagator(csr)
+    elif partition == "features":
         prop = FeaturePartitionedPropagator(csr, rank=rank, world_size=world, group=group,
                                             host_staging=staging)
     elif partition == "lines":
@@ -147,13 +157,71 @@ def _propagator(csr, group, partition, staging):
     return prop
 
 
+class ReplicatedPropagator:
+    """Every rank computes all of X_K itself: the single-GPU propagation, no
+    exchange -- one GPU's time at any world size, the floor the partitioned
+    candidates must beat for a replicated X_K."""
+
+    def __init__(self, csr):
+        self.csr = csr
+
+    def propagate(self, X0, K, out=None, output="replicated"):
+        if output != "replicated":
+            raise ValueError("ReplicatedPropagator: output='replicated' only")
+        from .propagate import propagate
+        return propagate(self.csr, X0, K, out=out)
+
+
+def _sync(X):
+    if X.is_cuda:
+        torch.cuda.synchronize(X.device)
+
+
+def _slowest(seconds, X, group):
+    """Max over the group's ranks of each rank's seconds (list), one all-reduce."""
+    dev = X.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.tensor(seconds, dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return [float(v) for v in t.cpu()]
+
+
+def auto_choice(csr, group, F, K):
+    """The auto partition's record for (adjacency, group, F, K) once chosen:
+    {"chosen": name, "seconds": {candidate: slowest rank's time}}, or None."""
+    return csr._plans.get(("auto", id(group), dist.get_world_size(group), int(F), int(K)))
+
+
 def precompute_group(csr, X, K, group):
     """X_K = S^K X on every rank of `group`, partitioned (the caller has
     checked shapes and devices).  Collective: every rank must call it with
-    the same adjacency and feature shape."""
+    the same adjacency and feature shape (the auto choice then agrees on every
+    rank: it is taken from the all-reduced times)."""
     staging = X.is_cuda and dist.get_backend(group) != "nccl"
-    prop = _propagator(csr, group, partition_name(dist.get_world_size(group)), staging)
-    return prop.propagate(X, K, output="replicated")
+    name = partition_name()
+    if name != "auto":
+        return _propagator(csr, group, name, staging).propagate(X, K, output="replicated")
+    world = dist.get_world_size(group)
+    key = ("auto", id(group), world, int(X.shape[1]), int(K))
+    rec = csr._plans.get(key)
+    if rec is not None:
+        return _propagator(csr, group, rec["chosen"], staging).propagate(X, K,
+                                                                          output="replicated")
+    # first call: warm every candidate, time one call of each (max over
+    # ranks), keep the fastest; its result is this call's
+    cands = list(AUTO_CANDIDATES)
+    secs, outs = [], {}
+    for c in cands:
+        prop = _propagator(csr, group, c, staging)
+        prop.propagate(X, K, output="replicated")
+        _sync(X)
+        t0 = time.perf_counter()
+        outs[c] = prop.propagate(X, K, output="replicated")
+        _sync(X)
+        secs.append(time.perf_counter() - t0)
+    slow = _slowest(secs, X, group)
+    best = min(range(len(cands)), key=lambda i: (slow[i], i))
+    csr._plans[key] = {"chosen": cands[best], "seconds": dict(zip(cands, slow))}
+    return outs[cands[best]]
 
 
 # ---------------------------------------------------------------------------
@@ -274,4 +342,4 @@ def feature_blocks(F, parts, align=4):
 
 __all__ = ["torchrun_env", "bind_local_device", "process_group", "precompute_group",
            "devices_from_env", "DeviceSet", "precompute_devices", "feature_blocks",
-           "PARTITIONS"]
+           "PARTITIONS", "AUTO_CANDIDATES", "ReplicatedPropagator", "auto_choice"]

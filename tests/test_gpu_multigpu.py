@@ -164,7 +164,7 @@ def test_mgpu_handles_survive_reinit(tiny_cases, oracle):
 # ---------------------------------------------------------------------------
 # sgc_precompute under torchrun, the reddit driver, bench.py self-launch
 
-@pytest.mark.parametrize("partition", ["features", "lines", "rows", "cyclic"])
+@pytest.mark.parametrize("partition", ["features", "lines", "rows", "cyclic", "replicate", "auto"])
 def test_sgc_precompute_under_torchrun_matches_one_gpu(tmp_path, partition):
     """Two torchrun ranks sharing the GPU (gloo, chosen by the drop-in because
     there are fewer GPUs than ranks) run the unchanged sgc_precompute on the
@@ -181,6 +181,22 @@ def test_sgc_precompute_under_torchrun_matches_one_gpu(tmp_path, partition):
     for rec in recs:
         assert rec["world"] == 2 and rec["backend"] == "gloo" and rec["repeat_equal"]
         assert rec["sha"] == want
+
+
+def test_rccl_exchange_paths_world1():
+    """The RCCL calls of the feature and line partitions on this one-GPU box
+    (tests/rank_rccl_world1.py): a one-rank nccl group with the propagators'
+    one-rank shortcuts turned off (force_collectives), so the in-place async
+    all-gathers of the last hop's row chunks, their waits on the compute
+    stream, the block-copy unpack and the line partition's tail-stream gather
+    pattern all run through RCCL; X_K equals one GPU's bit for bit.  (RCCL
+    refuses two ranks on one GPU, so this is as far as RCCL runs here.)"""
+    r = _torchrun(1, ["tests/rank_rccl_world1.py", "20000"], timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _last_json(r.stdout)
+    assert rec["backend"] == "nccl" and rec["world"] == 1, rec
+    assert rec["features_replicated_equal"] and rec["lines_replicated_equal"], rec
+    assert rec["lines_sharded_equal"] and rec["tail_stream_pattern_ok"], rec
 
 
 def test_reddit_driver_runs_under_torchrun():
@@ -232,7 +248,8 @@ def dist_cache(tmp_path_factory):
     ("reddit", "features", []),
     ("reddit", "lines", ["--also-replicated"]),
     ("reddit", "tiles", ["--col-blocks", "2"]),
-    ("rmat", "rows", [])])
+    ("rmat", "rows", []),
+    ("rmat", "lines", [])])  # the P = 8 layout at F = 256: one 32-float line per rank
 def test_p8_partition_full_size_bit_exact(dist_cache, shape, partition, extra):
     r = _torchrun(8, ["scripts/dist_check.py", "--shape", shape, "--partition", partition,
                       "--cache", dist_cache, *extra], timeout=840)

@@ -524,7 +524,8 @@ def test_kernel_timing_hooks(tiny_cases, fuse):
 
 
 @pytest.mark.parametrize("M,K,C", [(1, 3, 1), (140, 1433, 7), (333, 602, 41), (1000, 500, 3),
-                                   (77, 64, 64), (50, 130, 100), (2048, 602, 41)])
+                                   (77, 64, 64), (50, 130, 100), (2048, 602, 41), (8192, 602, 41),
+                                   (5000, 1433, 7), (4096, 3703, 6), (6000, 500, 3)])
 def test_linear_mfma_vs_torch_fp32(M, K, C):
     from sgc_amd.propagate import linear
     g = torch.Generator().manual_seed(M * 7 + K)
@@ -603,6 +604,67 @@ def test_linear_stream_edges(M, K, C, ld_extra, ck):
     finally:
         lib.sgc_set_tuning(b"linear_kernel", 0)
         lib.sgc_set_tuning(b"linear_ck", prev_ck)
+
+
+@pytest.mark.parametrize("M,K,C,ld_extra", [(129, 602, 41, 6), (300, 33, 17, 1), (257, 31, 3, 1),
+                                            (128, 64, 64, 32), (1, 1, 1, 1), (1000, 333, 20, 0),
+                                            (70000, 602, 41, 0), (66000, 100, 48, 4),
+                                            (4099, 602, 42, 2)])
+def test_linear_split_edges(M, K, C, ld_extra):
+    """The split-bf16 streaming forward (linear_split_kernel, forced): every
+    operand split exactly into three bf16 pieces, six products on
+    v_mfma_f32_16x16x32_bf16, within the fp32 tolerance of fp64 torch.  X's
+    16-B loads at 8-B (ld = 602, the Reddit-train layout) and 4-B (ld = 333)
+    row alignment, 8 lanes per row then a DPP exchange; rows past M read
+    zeros; the last chunk's k >= K are zeroed (X holds infinities there);
+    class tiles with rows past C; M = 70,000 / 66,000 give waves more than one
+    tile, so the chunk stream crosses tile boundaries; C = 42 at K = 602 is
+    the largest W image that fits LDS."""
+    from sgc_amd import _lib
+    from sgc_amd.propagate import linear
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + K + C + 1)
+    Xf = torch.full((M, K + ld_extra), float("inf"))
+    Xf[:, :K] = torch.randn((M, K), generator=g)
+    W = torch.randn((C, K), generator=g) * 0.05
+    b = torch.randn(C, generator=g)
+    ref = torch.nn.functional.linear(Xf[:, :K].double(), W.double(), b.double())
+    tol = 1e-5 * max(1.0, ref.abs().max().item())
+    _lib.check(lib.sgc_set_tuning(b"linear_kernel", 5), "set_tuning")
+    try:
+        Xd = Xf.to(DEV)[:, :K]
+        name = lib.sgc_linear_kernel_name(M, K, Xd.stride(0), C, _lib.ptr(Xd)).decode()
+        assert name.startswith("linear_split_kernel"), name
+        Y = linear(Xd, W.to(DEV), b.to(DEV)).cpu().double()
+        torch.testing.assert_close(Y, ref, rtol=1e-5, atol=tol)
+        Yn = linear(Xd, W.to(DEV), None).cpu().double()
+        torch.testing.assert_close(Yn, ref - b.double(), rtol=1e-5, atol=tol)
+    finally:
+        lib.sgc_set_tuning(b"linear_kernel", 0)
+
+
+def test_linear_split_precision_vs_fp32_mfma():
+    """The split products keep fp32 precision: at the Reddit-train width the
+    split kernel's largest error against fp64 is within 2x the fp32 MFMA
+    streaming kernel's (both far inside the 1e-5 tolerance), on data with a
+    wide exponent range."""
+    from sgc_amd import _lib
+    from sgc_amd.propagate import linear
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn((8192, 602), generator=g) * torch.exp(2 * torch.randn((8192, 1), generator=g))
+    W = torch.randn((41, 602), generator=g) * 0.05
+    ref = torch.nn.functional.linear(X.double(), W.double())
+    errs = {}
+    try:
+        for kern in (2, 5):
+            _lib.check(lib.sgc_set_tuning(b"linear_kernel", kern), "set_tuning")
+            Y = linear(X.to(DEV), W.to(DEV)).cpu().double()
+            errs[kern] = ((Y - ref).abs() / (X.double().abs() @ W.double().abs().t())).max().item()
+    finally:
+        lib.sgc_set_tuning(b"linear_kernel", 0)
+    assert errs[5] <= 2 * errs[2] + 1e-8, errs
+    assert errs[5] < 1e-6, errs
 
 
 def test_sgc_model_autograd_matches_torch():

@@ -37,8 +37,10 @@ def _torchrun_like_worker(rank, world, port, case, K, partition, q):
         X = torch.from_numpy(case["X"])
         out, secs = sgc_precompute(X, adj, K)
         again, _ = sgc_precompute(X, adj, K)  # cached partition, buffers reused
+        from sgc_amd.multigpu import auto_choice
+        rec = auto_choice(adj._sgc_amd_csr[1], dist.group.WORLD, X.shape[1], K)
         q.put((rank, out.numpy().copy(), bool(torch.equal(out, again)), dist.get_world_size(),
-               secs >= 0))
+               secs >= 0, None if rec is None else rec["chosen"]))
     finally:
         import torch.distributed as dist2
         if dist2.is_initialized():
@@ -51,7 +53,9 @@ def _torchrun_like_worker(rank, world, port, case, K, partition, q):
     (2, "norm_n48_F65", 2, "rows"), (3, "norm_n48_F130", 2, "rows"),
     (2, "hub1000_F130", 2, "cyclic"), (4, "norm_n48_F65", 3, "cyclic"),
     (2, "isolated_F17", 1, "features"), (2, "norm_n48_F602", 2, "lines"),
-    (3, "hub1000_F130", 2, "lines"), (4, "norm_n48_F602", 2, "auto")])
+    (3, "hub1000_F130", 2, "lines"), (4, "norm_n48_F602", 2, "auto"),
+    (2, "norm_n48_F602", 2, "replicate"), (3, "hub1000_F130", 2, "replicate"),
+    (2, "hub1000_F130", 2, "auto"), (3, "raw_unsorted_dups_F7", 2, "auto")])
 def test_sgc_precompute_under_torchrun_env(tiny_cases, world, name, K, partition):
     case = tiny_cases[name]
     ctx = mp.get_context("spawn")
@@ -67,10 +71,16 @@ def test_sgc_precompute_under_torchrun_env(tiny_cases, world, name, K, partition
         assert p.exitcode == 0
     want = case[f"Y{K}"]
     for r in range(world):
-        out, stable, ws, timed = got[r]
+        out, stable, ws, timed, chosen = got[r]
         assert ws == world and stable and timed
         assert out.shape == want.shape
         assert np.array_equal(out.view(np.uint32), want.view(np.uint32)), (partition, r)
+        # auto: every rank keeps the same candidate (chosen from all-reduced times)
+        if partition == "auto":
+            from sgc_amd.multigpu import AUTO_CANDIDATES
+            assert chosen in AUTO_CANDIDATES and chosen == got[0][4], (r, chosen, got[0][4])
+        else:
+            assert chosen is None
 
 
 def test_single_process_is_untouched(monkeypatch):
@@ -107,7 +117,10 @@ def test_partition_name_checked(monkeypatch):
         multigpu.partition_name()
     monkeypatch.delenv("SGC_AMD_PARTITION")
     assert multigpu.partition_name() == "auto"
-    assert [multigpu.partition_name(w) for w in (2, 3, 4, 8)] == ["features", "features",
-                                                                   "lines", "lines"]
+    # auto is chosen by measured time on the first call, whatever the world size
+    assert [multigpu.partition_name(w) for w in (2, 3, 4, 8)] == ["auto"] * 4
+    assert multigpu.AUTO_CANDIDATES[0] == "replicate"
+    monkeypatch.setenv("SGC_AMD_PARTITION", "replicate")
+    assert multigpu.partition_name(2) == "replicate"
     monkeypatch.setenv("SGC_AMD_PARTITION", "rows")
     assert multigpu.partition_name(8) == "rows"
