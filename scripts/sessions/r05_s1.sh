@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-5 session 1: classifier A/B + tests, pad A/B, replicated rehearsal.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 2
+mkdir -p gpurun_out
+( while sleep 45; do date +%T >> gpurun_out/heartbeat.log; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+timeout -k 10 120 python scripts/linear_ab.py --kernels 2,5,6,7,8 --rounds 3 > gpurun_out/linear_ab.log 2>&1 || exit $?
+timeout -k 10 200 python -u -m pytest tests/test_gpu_parity.py -x -q -k "linear" --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/lin_tests.log 2>&1
+rc=$?; echo "lin_tests rc=$rc"; [ $rc -gt 1 ] && exit $rc
+timeout -k 10 300 python scripts/pad_ab.py > gpurun_out/pad_ab.log 2>&1 || exit $?
+timeout -k 10 600 python scripts/replicated_rehearsal.py > gpurun_out/replicated_rehearsal.log 2>&1 || exit $?
+echo done

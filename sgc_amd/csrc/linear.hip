@@ -283,8 +283,9 @@ __global__ __launch_bounds__(64 * kStreamWaves) void linear_stream_kernel(
 // dropped ml, lm, ll are below 2^-25 of |x||w|) -- on v_mfma_f32_16x16x32_bf16,
 // whose bf16 x bf16 products are exact in its fp32 sums: 6/16 of the fp32 MFMA
 // time, so the X stream alone sets the pace.  Tolerance parity with fp32
-// (test_linear_split_*); X values past +-3.39e38 (bf16's largest finite) are
-// not supported.
+// (test_linear_split_*).  Finite X and W only: an infinite x gives NaN (its
+// residual x - h is inf - inf), where torch gives +-inf or NaN; values past
+// bf16's largest finite (+-3.39e38) likewise.
 // * X stream: per 32-k chunk of a 16-row tile a lane issues two b128 loads,
 //   each wave-instruction reading 128 contiguous bytes of each of 8 rows (8
 //   lanes per row): instruction 0 rows 0-7, instruction 1 rows 8-15, lane
@@ -293,30 +294,45 @@ __global__ __launch_bounds__(64 * kStreamWaves) void linear_stream_kernel(
 //   loaded directly) streamed at 2.4-3.2 TB/s, this one at 5.5-5.8
 //   (scripts/micro/stream_shape.hip, profiles/r05/stream_shape.log).  One DPP
 //   row_ror:8 exchange per register then gives lane (j, kg) floats 8kg..8kg+7
-//   of row j -- the bf16 16x16x32 A operand, k in natural order.
-// * W's three bf16 images (C rows each, not padded to the class tile; rows
-//   past C read as zeros) stay in LDS for the whole persistent launch, 16-B
-//   granules XOR-swizzled per 128-k window (conflict-free ds_read_b128).
-// * Two accumulator sets per class tile, the hh products and the five small
-//   ones, summed at the store.
-constexpr int kSplitDepth = 4;  // chunks in flight per wave
+//   of row j -- the bf16 16x16x32 B operand, k in natural order.
+// * D = W . X^T (W the A operand): a lane's accumulator holds four
+//   consecutive classes of one row, so a tile's output is b128 stores.
+// * W's pieces stay in LDS for the whole persistent launch in MFMA-operand
+//   order: per 32-k chunk, per class tile, each lane's three 16-B operands
+//   side by side (48 B per lane: conflict-free b128 reads, the piece and the
+//   tile as immediate offsets, one address add per chunk); the last class
+//   tile keeps only its Cl real classes (+ one zero granule for the lanes
+//   past them), which is what fits C = 41 at K = 602 (150 KB).  The image is
+//   built in-kernel after the first X loads are in flight.
+// * The ring of D chunks per wave runs across tiles with compile-time slots
+//   (a rolled ring moved registers and selected slots at run time: ~100 extra
+//   VALU per chunk).
+constexpr int kSplitDepth = 4;  // chunks in flight per wave (the ring's slots)
+#ifndef SGC_SPLIT_HELD
+#define SGC_SPLIT_HELD 6
+#endif
+// Finished tiles a wave holds in registers before it stores them (at NT = 3;
+// more at NT <= 2, fewer at NT = 4): stores count in the same vmcnt as the X
+// loads, so stores issued while the loads stream make the next chunks'
+// counted waits drain the ring.  Held, a wave stores after its last load
+// (~4.7 tiles per wave at the Reddit-train shape; a seventh flushes the six).
+constexpr int kSplitHeld = SGC_SPLIT_HELD;
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int U> struct SlotC { static constexpr int value = U; };
 
 __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
     const bf16x2_t v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32 (RNE)
     return __builtin_bit_cast(uint32_t, v);
 }
 
-// (a, b) -> packed hi / mid / lo bf16 pairs with a == hi + mid + lo exactly.
-// A non-finite residual (x infinite) is taken as 0, so x = +-inf keeps its
-// hi . w products as the fp32 sum would.
+// (a, b) -> packed hi / mid / lo bf16 pairs with a == hi + mid + lo exactly
+// (finite a, b).
 __device__ __forceinline__ void split3(float a, float b, uint32_t &h, uint32_t &m, uint32_t &l) {
     h = pk_bf16(a, b);
-    float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
-    ra = __builtin_fabsf(ra) <= 3.402823466e38f ? ra : 0.0f;
-    rb = __builtin_fabsf(rb) <= 3.402823466e38f ? rb : 0.0f;
+    const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
     m = pk_bf16(ra, rb);
     l = pk_bf16(ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u));
 }
@@ -326,44 +342,28 @@ __device__ __forceinline__ float ror8(float x) {  // lane j of each 16-lane row 
         float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128, 0xf, 0xf, false));
 }
 
-// DIAG 1: the loads and the exchange only (the X stream's own time).
+// W image geometry (host and device): bytes per chunk for NT class tiles, the
+// last holding Cl classes.
+__host__ __device__ constexpr int split_chunk_bytes(int NT, int Cl) {
+    return (NT - 1) * 3072 + (4 * Cl + 1) * 48;
+}
+
+// DIAG (diagnostics, sgc_set_tuning("linear_kernel", 6 / 7 / 8)): 1 = the
+// loads, the exchange and the stores without the split and the MFMAs; 2 = 1
+// without the stores; 3 = everything but the stores.
 template <int NT, int NW, int DIAG = 0>
 __global__ __launch_bounds__(64 * NW) void linear_split_kernel(
     const float *__restrict__ X, int64_t ldx, const float *__restrict__ W,
-    const float *__restrict__ b, float *__restrict__ Y, int64_t ldy, int M, int K, int C, int S) {
+    const float *__restrict__ b, float *__restrict__ Y, int64_t ldy, int M, int K, int C) {
     typedef float f4 __attribute__((ext_vector_type(4)));
-    // image p (0 hi, 1 mid, 2 lo), row r < C: granules [(p * C + r) * S, + S);
-    // granule q (k = 8q .. 8q + 7) of row r at (q & ~15) | ((q ^ r) & 15)
     extern __shared__ __attribute__((aligned(16))) u32x4 sgr[];
+    char *const lds = reinterpret_cast<char *>(sgr);
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, kg = lane >> 4;
-    for (int base = threadIdx.x; base < C * S; base += 4 * 64 * NW) {
-        float v[4][8];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int idx = base + u * 64 * NW;
-            const int r = idx / S, q = idx - r * S;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const int k = 8 * q + e;
-                v[u][e] = (idx < C * S && k < K) ? W[(int64_t)r * K + k] : 0.0f;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int idx = base + u * 64 * NW;
-            if (idx >= C * S) break;
-            const int r = idx / S, q = idx - r * S;
-            uint32_t h[4], m[4], l[4];
-#pragma unroll
-            for (int p = 0; p < 4; ++p) split3(v[u][2 * p], v[u][2 * p + 1], h[p], m[p], l[p]);
-            const int slot = (q & ~15) | ((q ^ r) & 15);
-            sgr[(0 * C + r) * S + slot] = u32x4{h[0], h[1], h[2], h[3]};
-            sgr[(1 * C + r) * S + slot] = u32x4{m[0], m[1], m[2], m[3]};
-            sgr[(2 * C + r) * S + slot] = u32x4{l[0], l[1], l[2], l[3]};
-        }
-    }
-    int *next = reinterpret_cast<int *>(sgr + 3 * C * S);
+    const int NC = (K + 31) / 32;         // chunks per tile
+    const int Cl = C - (NT - 1) * 16;     // classes of the last tile, 1..16
+    const int cstride = split_chunk_bytes(NT, Cl);
+    int *next = reinterpret_cast<int *>(lds + NC * cstride);
     if (threadIdx.x == 0) *next = 0;
     __syncthreads();
     const int n_tiles = (M + 15) >> 4;
@@ -374,7 +374,6 @@ __global__ __launch_bounds__(64 * NW) void linear_split_kernel(
         const int t = (int)blockIdx.x + (int)gridDim.x * m;
         return t < n_tiles ? t : -1;
     };
-    const int NC = (K + 31) / 32;  // chunks per tile
     const auto xd = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float *>(X), 0, (int)((int64_t)M * ldx * 4), 0x00020000);  // < 2^31
     const uint32_t seg = 16u * (2 * kg + (j >> 3));
@@ -388,121 +387,218 @@ __global__ __launch_bounds__(64 * NW) void linear_split_kernel(
     };
     rows_of(ltile);
     constexpr int D = kSplitDepth;
+    static_assert(D == 4, "the ring's slots are unrolled by hand below");
     f4 xa[D], xb[D];
     int stile[D], sc[D];
     // Both loads are issued on every path (past the last tile their offsets
     // are out of range: zeros, no memory traffic), so every path has the same
-    // loads in flight and the compiler's counted waits stay vmcnt(2 (D - 1))
-    // instead of draining the ring (vmcnt(0)) at each chunk.
-    auto load = [&](int slot) {
-        stile[slot] = ltile;
-        sc[slot] = lc;
+    // loads in flight and the compiler's counted waits stay exact.
+    auto load = [&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        stile[u] = ltile;
+        sc[u] = lc;
         const uint32_t co = (uint32_t)lc * 128u;
-        xa[slot] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xd, lrow0 + co, 0, 0));
-        xb[slot] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xd, lrow1 + co, 0, 0));
+        xa[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xd, lrow0 + co, 0, 0));
+        xb[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(xd, lrow1 + co, 0, 0));
         if (ltile >= 0 && ++lc == NC) {
             lc = 0;
             ltile = grab();
             rows_of(ltile);
         }
     };
-    // the bias of the lane's classes, read before the stream starts (a global
-    // load in the loop would make the tile's stores wait for every X load)
-    float bias[NT];
+    // the ring's first chunks are in flight while W's image is built
+    load(SlotC<0>{});
+    load(SlotC<1>{});
+    load(SlotC<2>{});
+    load(SlotC<3>{});
+    {
+        // one unit = one lane's operand granule of one (chunk, class tile):
+        // 8 k of one class, split into its three pieces, stored side by side
+        const auto wd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(W), 0,
+                                                          (int)((int64_t)C * K * 4), 0x00020000);
+        const int full = (NT - 1) * 64, units = full + 4 * Cl + 1;
+        for (int idx = threadIdx.x; idx < NC * units; idx += 64 * NW) {
+            const int c = idx / units, w = idx - c * units;
+            int r = 0, kk = 0;
+            bool zero = false;
+            if (w < full) {
+                r = (w >> 6) * 16 + (w & 15);
+                kk = (w >> 4) & 3;
+            } else if (w < full + 4 * Cl) {
+                kk = (w - full) / Cl;
+                r = (NT - 1) * 16 + (w - full - kk * Cl);
+            } else {
+                zero = true;
+            }
+            const int k0 = c * 32 + 8 * kk;
+            float e[8];
 #pragma unroll
-    for (int n = 0; n < NT; ++n) bias[n] = (b && n * 16 + j < C) ? b[n * 16 + j] : 0.0f;
+            for (int q = 0; q < 8; ++q) {
+                const float x = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(
+                               wd, zero ? 0u : (uint32_t)(r * K + k0 + q) * 4u, 0, 0));
+                e[q] = (!zero && k0 + q < K) ? x : 0.0f;
+            }
+            uint32_t h[4], m[4], l[4];
 #pragma unroll
-    for (int u = 0; u < D; ++u) load(u);
+            for (int p = 0; p < 4; ++p) split3(e[2 * p], e[2 * p + 1], h[p], m[p], l[p]);
+            char *dst = lds + c * cstride + w * 48;
+            *reinterpret_cast<u32x4 *>(dst) = u32x4{h[0], h[1], h[2], h[3]};
+            *reinterpret_cast<u32x4 *>(dst + 16) = u32x4{m[0], m[1], m[2], m[3]};
+            *reinterpret_cast<u32x4 *>(dst + 32) = u32x4{l[0], l[1], l[2], l[3]};
+        }
+    }
+    __syncthreads();
+    // a lane's operand granules: full tile n at bfull + n * 3072, the last
+    // tile at blast (the zero granule for lanes past its Cl classes); piece p
+    // at + 16 p; chunk c at + c * cstride
+    const uint32_t bfull = (uint32_t)lane * 48u;
+    const uint32_t blast = (NT - 1) * 3072u + 48u * (uint32_t)(j < Cl ? kg * Cl + j : 4 * Cl);
+    // the bias of the lane's classes (n * 16 + 4 kg + r)
+    f4 bias[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int cl = n * 16 + 4 * kg + r;
+            bias[n][r] = (b && cl < C) ? b[cl] : 0.0f;
+        }
+    const auto yd = __builtin_amdgcn_make_buffer_rsrc(Y, 0, (int)((int64_t)M * ldy * 4),
+                                                      0x00020000);  // < 2^31
+    constexpr int PT = NT <= 2 ? kSplitHeld + 2 : NT == 3 ? kSplitHeld : kSplitHeld - 2;
+    f4 held[PT][NT];
+    uint32_t hrow[PT];
+    int nheld = 0;  // uniform
+    const int pcl = (NT - 1) * 16 + 4 * kg;  // the lane's last class group
+    const bool ppart = pcl + 4 > C;           // partial (or empty): b32 stores
+    // Y row offset -> its classes: full groups of four by b128, the partial
+    // last group by b32; every store issued, out-of-range offsets when empty
+    auto store_tile = [&](const f4 (&o)[NT], uint32_t yrow) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            const int cl0 = n * 16 + 4 * kg;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o[n]), yd,
+                                                   cl0 + 4 <= C ? yrow + 4u * cl0 : kOffOOB, 0, 0);
+        }
+        if (C < NT * 16) {  // uniform: a partial last class tile
+            // (the elements as separate values first: extracting them from
+            // the vector the b128 store took was miscompiled -- every b32
+            // store wrote element 0)
+            const u32x4 pe = __builtin_bit_cast(u32x4, o[NT - 1]);
+            const uint32_t e0 = pe.x, e1 = pe.y, e2 = pe.z, e3 = pe.w;
+            auto off = [&](int r) { return (ppart && pcl + r < C) ? yrow + 4u * (pcl + r) : kOffOOB; };
+            __builtin_amdgcn_raw_buffer_store_b32(e0, yd, off(0), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(e1, yd, off(1), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(e2, yd, off(2), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(e3, yd, off(3), 0, 0);
+        }
+    };
+    auto flush = [&]() {
+#pragma unroll
+        for (int t = 0; t < PT; ++t)
+            if (t < nheld) store_tile(held[t], hrow[t]);  // uniform
+        nheld = 0;
+    };
     f32x4 accH[NT], accL[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n) accH[n] = accL[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float diag_sum = 0.0f;
     const bool low = j < 8;
-    for (;;) {
+    auto step = [&](auto uc) -> bool {  // false: the stream is done (uniform)
+        constexpr int u = decltype(uc)::value;
+        const int tile = stile[u], c = sc[u];
+        if (tile < 0) return false;
+        // W operands of chunk c
+        u32x4 bw[NT][3];
+        {
+            const uint32_t coff = (uint32_t)c * (uint32_t)cstride;
+            const char *af = lds + bfull + coff;
+            const char *al = lds + blast + coff;
 #pragma unroll
-        for (int u = 0; u < D; ++u) {
-            const int tile = stile[u], c = sc[u];
-            if (tile < 0) return;  // wave-uniform: the stream is in order
-            // W operands of chunk c: granule 4c + kg of row n * 16 + j of each image
-            u32x4 bw[NT][3];
-            {
-                const int q = 4 * c + kg;
-                const int slot = (q & ~15) | ((q ^ j) & 15);
+            for (int n = 0; n < NT; ++n)
 #pragma unroll
-                for (int n = 0; n < NT; ++n) {
-                    const int r = n * 16 + j;
-#pragma unroll
-                    for (int p = 0; p < 3; ++p)
-                        bw[n][p] = (r < C) ? sgr[(p * C + r) * S + slot] : u32x4{0u, 0u, 0u, 0u};
-                }
-            }
-            const f4 A = xa[u], B = xb[u];
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float t = ror8(low ? B[e] : A[e]);
-                v[e] = low ? A[e] : t;
-                v[4 + e] = low ? t : B[e];
-            }
-            load(u);  // the chunk D ahead into the slot just consumed
-            if ((c + 1) * 32 > K) {  // the ragged last chunk (uniform)
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (c * 32 + 8 * kg + e >= K) v[e] = 0.0f;
-            }
-            if constexpr (DIAG == 1 || DIAG == 2) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) accH[0][e & 3] += v[e];
-            } else {
-                uint32_t ah[4], am[4], al[4];
-#pragma unroll
-                for (int p = 0; p < 4; ++p) split3(v[2 * p], v[2 * p + 1], ah[p], am[p], al[p]);
-                const bf16x8_t Ah = __builtin_bit_cast(bf16x8_t, u32x4{ah[0], ah[1], ah[2], ah[3]});
-                const bf16x8_t Am = __builtin_bit_cast(bf16x8_t, u32x4{am[0], am[1], am[2], am[3]});
-                const bf16x8_t Al = __builtin_bit_cast(bf16x8_t, u32x4{al[0], al[1], al[2], al[3]});
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-                    accH[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        Ah, __builtin_bit_cast(bf16x8_t, bw[n][0]), accH[n], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-                    accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        Ah, __builtin_bit_cast(bf16x8_t, bw[n][1]), accL[n], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-                    accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        Am, __builtin_bit_cast(bf16x8_t, bw[n][0]), accL[n], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-                    accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        Ah, __builtin_bit_cast(bf16x8_t, bw[n][2]), accL[n], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-                    accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        Al, __builtin_bit_cast(bf16x8_t, bw[n][0]), accL[n], 0, 0, 0);
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-                    accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        Am, __builtin_bit_cast(bf16x8_t, bw[n][1]), accL[n], 0, 0, 0);
-            }
-            if (DIAG >= 2 && c == NC - 1) {  // diagnostics without the Y stores
-                if (accH[0][0] == 12345.0f) Y[lane] = accH[0][1];
-                continue;
-            }
-            if (c == NC - 1) {  // tile done: D[4 kg + r][j] = row 4 kg + r, class n * 16 + j
-                const int m0 = tile * 16 + 4 * kg;
-#pragma unroll
-                for (int n = 0; n < NT; ++n) {
-                    const int cl = n * 16 + j;
-                    if (cl < C) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            if (m0 + r < M)
-                                Y[(int64_t)(m0 + r) * ldy + cl] = accH[n][r] + accL[n][r] + bias[n];
-                    }
-                    accH[n] = accL[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-                }
-            }
+                for (int p = 0; p < 3; ++p)
+                    bw[n][p] = *reinterpret_cast<const u32x4 *>(
+                        (n < NT - 1 ? af + n * 3072 : al) + 16 * p);
         }
+        const f4 A = xa[u], B = xb[u];
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float t = ror8(low ? B[e] : A[e]);
+            v[e] = low ? A[e] : t;
+            v[4 + e] = low ? t : B[e];
+        }
+        load(uc);  // the chunk D ahead into the slot just consumed
+        if ((c + 1) * 32 > K) {  // the ragged last chunk (uniform)
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (c * 32 + 8 * kg + e >= K) v[e] = 0.0f;
+        }
+        if constexpr (DIAG == 1 || DIAG == 2) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) accH[0][e & 3] += v[e];
+        } else {
+            uint32_t ah[4], am[4], al[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) split3(v[2 * p], v[2 * p + 1], ah[p], am[p], al[p]);
+            const bf16x8_t Xh = __builtin_bit_cast(bf16x8_t, u32x4{ah[0], ah[1], ah[2], ah[3]});
+            const bf16x8_t Xm = __builtin_bit_cast(bf16x8_t, u32x4{am[0], am[1], am[2], am[3]});
+            const bf16x8_t Xl = __builtin_bit_cast(bf16x8_t, u32x4{al[0], al[1], al[2], al[3]});
+            auto wb = [&](int n, int p) { return __builtin_bit_cast(bf16x8_t, bw[n][p]); };
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                accH[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb(n, 0), Xh, accH[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb(n, 1), Xh, accL[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb(n, 0), Xm, accL[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb(n, 2), Xh, accL[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb(n, 0), Xl, accL[n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+                accL[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb(n, 1), Xm, accL[n], 0, 0, 0);
+        }
+        if (c == NC - 1) {  // tile done: D[4 kg + r][j] = class n * 16 + 4 kg + r, row j
+            const int row = tile * 16 + j;  // rows past M: out-of-range offsets, dropped
+            const uint32_t yrow = row < M ? (uint32_t)((int64_t)row * ldy * 4) : kOffOOB;
+            if constexpr (DIAG >= 2) {  // diagnostics without the stores
+#pragma unroll
+                for (int n = 0; n < NT; ++n)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) diag_sum += accH[n][r] + accL[n][r];
+            } else {
+                if (nheld == PT) flush();
+#pragma unroll
+                for (int t = 0; t < PT; ++t)
+                    if (t == nheld) {  // uniform
+#pragma unroll
+                        for (int n = 0; n < NT; ++n) held[t][n] = accH[n] + accL[n] + bias[n];
+                        hrow[t] = yrow;
+                    }
+                ++nheld;
+            }
+#pragma unroll
+            for (int n = 0; n < NT; ++n) accH[n] = accL[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        return true;
+    };
+    for (;;) {
+        if (!step(SlotC<0>{})) break;
+        if (!step(SlotC<1>{})) break;
+        if (!step(SlotC<2>{})) break;
+        if (!step(SlotC<3>{})) break;
+    }
+    if constexpr (DIAG >= 2) {
+        if (diag_sum == 12345.0f) Y[lane] = diag_sum;  // keeps the work live
+    } else {
+        flush();
     }
 }
 
@@ -595,13 +691,16 @@ hipError_t launch_stream(const float *X, int64_t ldx, const float *W, const floa
 
 constexpr int kSplitWaves = 8;
 
-// Split-bf16 kernel: W's three images, C rows of S granules each, + the tile
-// counter; S covers the chunks' k rounded up to a 128-k swizzle window.
-inline int split_granules(int64_t K) { return (int)(((K + 31) / 32 * 4 + 15) / 16 * 16); }
-inline size_t split_lds(int64_t K, int C) { return (size_t)3 * C * split_granules(K) * 16 + 16; }
+// Split-bf16 kernel: W's operand image (split_chunk_bytes per 32-k chunk) +
+// the tile counter.
+inline size_t split_lds(int64_t K, int C) {
+    const int NT = (C + 15) / 16;
+    return (size_t)((K + 31) / 32) * split_chunk_bytes(NT, C - (NT - 1) * 16) + 16;
+}
 
-bool split_fits(int64_t M, int64_t K, int64_t ldx, int C) {
-    return split_lds(K, C) <= 160 * 1024 && M * ldx * 4 < INT32_MAX && K < (int64_t(1) << 24);
+bool split_fits(int64_t M, int64_t K, int64_t ldx, int64_t ldy, int C) {
+    return split_lds(K, C) <= 160 * 1024 && M * ldx * 4 < INT32_MAX && M * ldy * 4 < INT32_MAX &&
+           K * C < (int64_t(1) << 29);
 }
 
 template <int NT, int DIAG>
@@ -614,8 +713,7 @@ hipError_t launch_split(const float *X, int64_t ldx, const float *W, const float
     const int tiles = (M + 15) / 16;
     const int blocks = std::max(1, std::min(cus, tiles));
     hipLaunchKernelGGL((linear_split_kernel<NT, kSplitWaves, DIAG>), dim3((unsigned)blocks),
-                       dim3(64 * kSplitWaves), split_lds(K, C), s, X, ldx, W, b, Y, ldy, M, K, C,
-                       split_granules(K));
+                       dim3(64 * kSplitWaves), split_lds(K, C), s, X, ldx, W, b, Y, ldy, M, K, C);
     return hipGetLastError();
 }
 
@@ -630,10 +728,11 @@ bool stream_fits(int64_t M, int64_t K, int64_t ldx, int nt, const float *X, size
 // Which forward kernel a class block of cc <= 64 classes takes (the
 // diagnostic forms, tuning 3 / 4 / 6, count as their kernel).
 enum LinearChoice { kLinTile, kLinStream, kLinSplit };
-LinearChoice linear_choice(int64_t M, int64_t K, int64_t ldx, int cc, const float *X) {
+LinearChoice linear_choice(int64_t M, int64_t K, int64_t ldx, int64_t ldy, int cc,
+                           const float *X) {
     size_t lds = 0;
     const bool stream_ok = stream_fits(M, K, ldx, (cc + 15) / 16, X, &lds);
-    const bool split_ok = split_fits(M, K, ldx, cc);
+    const bool split_ok = split_fits(M, K, ldx, ldy, cc);
     if (g_linear_kernel >= 5 || (g_linear_kernel == 0 && split_ok && M >= 4096)) return kLinSplit;
     if (g_linear_kernel >= 2 || (g_linear_kernel == 0 && stream_ok && M >= 4096)) return kLinStream;
     return kLinTile;
@@ -645,7 +744,7 @@ const char *linear_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C, con
         "linear_stream_kernel (fp32 streaming, v_mfma_f32_16x16x4_f32)",
         "linear_split_kernel (split-bf16 streaming, v_mfma_f32_16x16x32_bf16 x 6 products)"};
     if (M <= 0 || K <= 0 || C <= 0 || ldx < K) return "none";
-    return names[linear_choice(M, K, ldx, (int)std::min<int64_t>(C, 64), X)];
+    return names[linear_choice(M, K, ldx, C, (int)std::min<int64_t>(C, 64), X)];
 }
 
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
@@ -668,8 +767,8 @@ int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *
         float *Yc = Y + c0;
         size_t lds = 0;
         const bool stream_ok = stream_fits(M, K, ldx, nt, X, &lds);
-        const bool split_ok = split_fits(M, K, ldx, cc);
-        if (linear_choice(M, K, ldx, cc, X) == kLinSplit) {
+        const bool split_ok = split_fits(M, K, ldx, ldy, cc);
+        if (linear_choice(M, K, ldx, ldy, cc, X) == kLinSplit) {
             SGC_REQUIRE(split_ok, SGC_EINVAL, "linear: split kernel preconditions not met");
             hipError_t e;
             const int diag = g_linear_kernel - 5;
@@ -697,7 +796,7 @@ int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *
             SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear launch failed: %s", hipGetErrorString(e));
             continue;
         }
-        if (linear_choice(M, K, ldx, cc, X) == kLinStream) {
+        if (linear_choice(M, K, ldx, ldy, cc, X) == kLinStream) {
             SGC_REQUIRE(stream_ok, SGC_EINVAL, "linear: streaming kernel preconditions not met");
             const int Kp = (int)((K + 31) / 32 * 32);
             const bool v4 = ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0;

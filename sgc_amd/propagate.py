@@ -586,6 +586,11 @@ def _needs_pad(X):
     return X.stride(0) % 32 != 0 or X.data_ptr() % 128 != 0
 
 
+# Override of pad_pays (None = the rule; True / False force the re-layout on
+# or off -- scripts/pad_ab.py times both, results bit-identical either way).
+PAD_X0 = None
+
+
 def pad_pays(csr, F):
     """Re-lay X_0 into 128-B rows before hop 1?  An unaligned row segment
     touches about one extra 128-B line per gathered row (32/F of the hop's
@@ -633,7 +638,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
     key = None
     if not native_loop and hop_hook is None:
         key = ("loop", X.data_ptr(), X.stride(0), F, int(K), out.data_ptr(), out.stride(0),
-               threshold, hub_threshold, bool(use_plan), G_rule, stream.value)
+               threshold, hub_threshold, bool(use_plan), G_rule, stream.value, PAD_X0)
         prep = csr._plans.get(key)
         if prep is not None:
             with torch.cuda.device(X.device):
@@ -675,7 +680,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                 ctypes.cast(ths, ctypes.c_void_p), ctypes.cast(pflags, ctypes.c_void_p),
                 _lib.ptr(ws), ws_bytes, stream), "propagate_groups_f32")
             return out
-        pad = _needs_pad(X) and pad_pays(csr, F)
+        pad = _needs_pad(X) and (pad_pays(csr, F) if PAD_X0 is None else bool(PAD_X0))
         # buffers actually used: the re-laid X_0 (if any) + up to two
         # ping-pong intermediates (the last hop writes `out`)
         n_bufs = min(2, int(pad) + min(K - 1, 2))
