@@ -14,9 +14,11 @@ synthetic Reddit-shape graph (232,965 nodes, 11,606,919 undirected edges,
 nnz(S) = 23,446,803, F = 602, K = 2), inputs resident in HBM.
 A "step" = one full K-hop propagation.  N > 1: `value` times the SAME call
 as N = 1 -- sgc_precompute(features, adj, K) on every rank under the process
-group (sgc_amd.multigpu: partitioned hops, every rank gets the whole X_K, as
-the reference returns it; partition SGC_AMD_PARTITION, default features);
-total work fixed, so scaling is "strong".  Beside it (`sharded_output`) the
+group (sgc_amd.multigpu: every rank gets the whole X_K, as the reference
+returns it; partition SGC_AMD_PARTITION, default "auto": the first call times
+replicate / features / lines on the node, max over ranks, and keeps the
+fastest -- `config.partition` names it, `config.auto_seconds` lists the
+times); total work fixed, so scaling is "strong".  Beside it (`sharded_output`) the
 partitioned propagator with sharded output (sgc_amd.distributed):
   --partition rows  S row-partitioned (nnz-balanced row blocks, SURVEY.md
                 8(e)); RCCL all-gather of X_k after each hop that feeds another,
@@ -277,10 +279,12 @@ def mean_or_none(v):
     return float(np.mean(v)) if v else None
 
 
-def timed(step, steps, warmup, distributed, dev, on_start=None, on_stop=None):
+def timed(step, steps, warmup, distributed, dev, on_start=None, on_stop=None, events=True):
     """W untimed warm-ups, then exactly `steps` steps between
     synchronise + barrier pairs; returns (max-over-ranks elapsed s, per-step
-    ms from events on the current stream)."""
+    ms from events on the current stream -- [] with events=False: the value
+    run takes no per-step events, which cost host time per step that a
+    Pubmed-shape call (~0.1 ms) would otherwise carry)."""
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -290,12 +294,16 @@ def timed(step, steps, warmup, distributed, dev, on_start=None, on_stop=None):
     if on_start:
         on_start()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(steps)]
+           for _ in range(steps)] if events else []
     t0 = time.perf_counter()
-    for s, e in evs:
-        s.record()
-        step()
-        e.record()
+    if events:
+        for s, e in evs:
+            s.record()
+            step()
+            e.record()
+    else:
+        for _ in range(steps):
+            step()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -355,13 +363,14 @@ def single_gpu_shape(shape, args, dev, lib_sha, steps, warmup, S=None, X_host=No
     # same number of steps again with the library's per-launch events on (the
     # roofline's kernel times) -- at Cora shape those events alone would add
     # more host time per step than the two hops take on the GPU
-    elapsed, step_ms, _ = timed(step, steps, warmup, False, dev)
-    elapsed_i, _, (hop_ms, light, hub, kernel) = timed(
+    elapsed, _, _ = timed(step, steps, warmup, False, dev, events=False)
+    elapsed_i, step_ms, (hop_ms, light, hub, kernel) = timed(
         step, steps, 1, False, dev, on_start=launches.start, on_stop=launches.stop)
     hop_mean = float(np.mean(hop_ms))
     rec = {"value": K * nnz * steps / elapsed, "unit": "edges/s",
            "ms_per_step": elapsed * 1e3 / steps,
            "ms_per_step_median": float(np.median(step_ms)),
+           "ms_per_step_median_basis": "per-step events of the instrumented run",
            "ms_per_step_events": [round(v, 4) for v in step_ms],
            "ms_per_step_instrumented": elapsed_i * 1e3 / steps,
            "steps": steps, "warmup": warmup,
@@ -707,13 +716,16 @@ def main():
 
     def public_step():
         return sgc_precompute(X0, adj, K)[0]
-    elapsed, step_ms, _ = timed(public_step, args.steps, args.warmup, True, dev)
+    elapsed, _, _ = timed(public_step, args.steps, args.warmup, True, dev, events=False)
     # the same steps again with the library's per-launch events (rank 0's
     # launches: the roofline's kernel and times; label from the library)
-    elapsed_i, _, extra = timed(public_step, args.steps, 1, True, dev,
-                                on_start=launches.start if rank == 0 else None,
-                                on_stop=launches.stop if rank == 0 else None)
+    elapsed_i, step_ms, extra = timed(public_step, args.steps, 1, True, dev,
+                                      on_start=launches.start if rank == 0 else None,
+                                      on_stop=launches.stop if rank == 0 else None)
     span, light, hub, kernel = extra if extra else (None, None, None, None)
+    auto_rec = multigpu.auto_choice(adj._sgc_amd_csr[1], dist.group.WORLD, F, K)
+    if partition == "auto" and auto_rec is not None:
+        partition = auto_rec["chosen"]
     sharded = None
     if args.sharded_steps > 0:
         # beside it: the partitioned propagator with SHARDED output (each rank
@@ -757,7 +769,8 @@ def main():
                     "config": {"workload": f"{args.shape}-shape sgc_precompute K={K}", "nodes": n,
                                "undirected_edges": spec["edges"], "nnz": nnz, "features": F,
                                "hops": K, "parallelism": par, "output": "replicated",
-                               "partition": partition},
+                               "partition": partition,
+                               "auto_seconds": None if auto_rec is None else auto_rec["seconds"]},
                     "timed_call": "sgc_precompute(features, adj, K) (sgc_amd.utils, the drop-in), "
                                   "every rank, the same call as N = 1",
                     "first_call_seconds": round(first_pub, 4),
@@ -769,7 +782,10 @@ def main():
             # as N = 1's `compulsory_frac`) over the launches' summed spans
             # (launches on concurrent streams counted in full: conservative)
             cb = None
-            if partition == "features":
+            if partition == "replicate":
+                cb = K * (4 * (n + 1) + 8 * nnz + 8 * F * n)
+                unit = f"rank 0's K hops over all {n} rows at all {F} columns (replicate)"
+            elif partition == "features":
                 w = int(fb[1] - fb[0])
                 cb = K * (4 * (n + 1) + 8 * nnz + 8 * w * n)
                 unit = f"rank 0's K hops over all {n} rows at its {w}-column block"

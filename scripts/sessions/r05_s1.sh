@@ -10,4 +10,6 @@ timeout -k 10 200 python -u -m pytest tests/test_gpu_parity.py -x -q -k "linear"
 rc=$?; echo "lin_tests rc=$rc"; [ $rc -gt 1 ] && exit $rc
 timeout -k 10 300 python scripts/pad_ab.py > gpurun_out/pad_ab.log 2>&1 || exit $?
 timeout -k 10 600 python scripts/replicated_rehearsal.py > gpurun_out/replicated_rehearsal.log 2>&1 || exit $?
+
+timeout -k 10 200 python scripts/host_breakdown.py > gpurun_out/host_breakdown.log 2>&1
 echo done

@@ -3,7 +3,9 @@ reference's normalization.py.
 
 The values of S decide the arithmetic of the whole hot path, so this module
 reproduces the reference's numbers bit for bit (pinned by
-tests/test_normalization.py against fixtures made with the reference):
+tests/test_dropin.py::test_aug_normalized_adjacency_matches_reference against
+the reference module itself, and on the device by tests/test_gpu_normalize.py
+against the reference's S hashes):
 
 * aug_normalized_adjacency (reference normalization.py:5-12):
   S = D^-1/2 (A + I) D^-1/2 with D = rowsum(A + I), all in fp64;

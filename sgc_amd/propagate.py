@@ -233,12 +233,18 @@ class DeviceCSR:
                                           self.status) for g in range(G)]
         return self._plans[key]
 
+    def release_prepared(self):
+        """Free propagate()'s prepared loops on this adjacency (each keeps its
+        launch arguments and up to PREPARED_LOOP_MAX_BYTES of intermediates;
+        at most PREPARED_LOOPS_KEPT of them).  The next call prepares again."""
+        for key in [k for k in self._plans if isinstance(k, tuple) and k[:1] == ("loop",)]:
+            del self._plans[key]
+
     def drop_groups(self):
         """Free the cached column-group copies of S (and their plans): one
         more col/val copy per G (188 MB at Reddit shape).  They are rebuilt
         on the next launch that uses them."""
-        for key in [k for k in self._plans if isinstance(k, tuple) and k[:1] == ("loop",)]:
-            del self._plans[key]  # prepared loops hold the groups' pointers
+        self.release_prepared()  # prepared loops hold the groups' pointers
         for key in [k for k in self._plans if isinstance(k, tuple) and k[:1] == ("groups",)]:
             for part in self._plans.pop(key):
                 part._plans.clear()
@@ -603,7 +609,7 @@ def pad_pays(csr, F):
 
 
 def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, threshold=None,
-              hop_hook=None, native_loop=False, hub_threshold=None):
+              hop_hook=None, native_loop=False, hub_threshold=None, prepare=True):
     """X_K = S^K X on the device (K >= 1); asynchronous on the current stream.
 
     Mirrors sgc_propagate_f32: X is first re-laid into 128-B aligned rows when
@@ -612,7 +618,9 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
     always copies), hops ping-pong between two aligned buffers, the
     last hop writes the contiguous [N, F] result.  hop_hook(phase, h) is called
     around each hop's launch ("start"/"end", for event timing).
-    native_loop=True runs the same loop inside the C ABI call instead."""
+    native_loop=True runs the same loop inside the C ABI call instead.
+    prepare=False neither replays nor keeps a prepared loop (GraphedPropagation's
+    warm-up and capture; nothing is kept under a stream capture either)."""
     X = check_propagation_inputs(csr, X)
     n, F = X.shape
     if out is None:
@@ -636,7 +644,8 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
     # the Python loop's ctypes calls are prepared once per (X, out, K, stream,
     # schedule) and replayed, with the intermediates kept with them
     key = None
-    if not native_loop and hop_hook is None:
+    if (not native_loop and hop_hook is None and prepare and
+            not torch.cuda.is_current_stream_capturing()):
         key = ("loop", X.data_ptr(), X.stride(0), F, int(K), out.data_ptr(), out.stride(0),
                threshold, hub_threshold, bool(use_plan), G_rule, stream.value, PAD_X0)
         prep = csr._plans.get(key)
@@ -753,13 +762,13 @@ class GraphedPropagation:
         csr.plan(0, n, threshold, hub_threshold, F)  # synchronous: never inside the capture
         side = torch.cuda.Stream(device=csr.device)
         side.wait_stream(torch.cuda.current_stream(csr.device))
-        with torch.cuda.stream(side):
-            propagate(csr, self.x_in, self.K, out=self.out, **kw)
+        with torch.cuda.stream(side):  # (no prepared loop kept for the side stream)
+            propagate(csr, self.x_in, self.K, out=self.out, prepare=False, **kw)
         torch.cuda.current_stream(csr.device).wait_stream(side)
         torch.cuda.synchronize(csr.device)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            propagate(csr, self.x_in, self.K, out=self.out, **kw)
+            propagate(csr, self.x_in, self.K, out=self.out, prepare=False, **kw)
 
     def run(self, X: torch.Tensor) -> torch.Tensor:
         X = _check_features(X, self.csr)

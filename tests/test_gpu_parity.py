@@ -515,12 +515,41 @@ def test_kernel_timing_hooks(tiny_cases, fuse):
         lib.sgc_set_tuning(b"hub_fuse", 1)
     light, hub = collect_kernel_timing()
     assert len(light) == 3 and all(t > 0 for t in light)
-    if fuse:  # hop 2 (X_1 in the engine's 16-B-lane rows) fused; hop 1 reads X_0 (F = 130) with 8-B lanes
-        assert hub[1] is None and hub[2] is None
+    if fuse:
+        # hop 2 (X_1 in the engine's 16-B-lane rows) fused; hop 1 reads the
+        # caller's X_0 (F = 130: 8-B lanes), which the fused launch cannot
+        # take, so its hub rows run just before the light launch
+        assert hub[0] > 0 and hub[1] is None and hub[2] is None
     else:
         assert hub[0] > 0 and hub[1] > 0 and hub[2] is None
     assert bits_equal(out.cpu().numpy(), c["Y2"])
     assert collect_kernel_timing() == ([], [])
+
+
+def test_hub_fusion_hop1_with_16B_rows(tiny_cases, oracle):
+    """Hop 1 fuses its hub rows too when the caller's X_0 gives 16-B lanes
+    (F % 4 == 0, 16-B aligned rows -- Pubmed's F = 500): no hub launch on any
+    hop, bit-exact against the oracle."""
+    from sgc_amd import _lib
+    from sgc_amd.propagate import DeviceCSR, collect_kernel_timing, kernel_timing, propagate
+    lib = _lib.load()
+    c = tiny_cases["hub1000_F130"]
+    n = int(c["n"])
+    X0 = np.ascontiguousarray(c["X"][:, :128])
+    rp, ci, va = oracle.coo_to_csr(n, n, c["rows"], c["cols"], c["vals"])
+    want = oracle.propagate(rp, ci, va, X0, 2)
+    csr = DeviceCSR.from_torch(coo_cuda(c))
+    X = torch.from_numpy(X0).to(DEV)
+    collect_kernel_timing()
+    _lib.check(lib.sgc_set_tuning(b"hub_fuse", 1), "set_tuning")
+    kernel_timing(True)
+    try:
+        out = propagate(csr, X, 2, threshold=3, hub_threshold=5)
+    finally:
+        kernel_timing(False)
+    light, hub = collect_kernel_timing()
+    assert len(light) == 2 and hub == [None, None], hub
+    assert bits_equal(out.cpu().numpy(), want)
 
 
 @pytest.mark.parametrize("M,K,C", [(1, 3, 1), (140, 1433, 7), (333, 602, 41), (1000, 500, 3),
