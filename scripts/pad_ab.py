@@ -19,7 +19,11 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from sgc_amd import graphs, propagate as P  # noqa: E402
+import importlib  # noqa: E402
+
+from sgc_amd import graphs  # noqa: E402
+
+P = importlib.import_module("sgc_amd.propagate")  # the module (sgc_amd.propagate is also a function name)
 
 
 def main():

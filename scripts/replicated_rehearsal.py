@@ -42,9 +42,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from sgc_amd import graphs  # noqa: E402
-from sgc_amd.distributed import (FeaturePartitionedPropagator, LinePartitionedPropagator,  # noqa: E402
-                                 _copy_blocks, feature_bounds, line_bounds, make_shard,
-                                 row_chunks)
+from sgc_amd.distributed import (REPLICATED_CHUNKS, FeaturePartitionedPropagator,  # noqa: E402
+                                 LinePartitionedPropagator, _copy_blocks, feature_bounds,
+                                 line_bounds, make_shard, replicated_chunks)
 from sgc_amd.propagate import DeviceCSR, propagate  # noqa: E402
 
 
@@ -70,6 +70,12 @@ class LocalFeatures(_Local, FeaturePartitionedPropagator):
     def _all_to_all(self, recv, send):
         recv.copy_(send)
         return None
+
+    def _exchange_pair(self, send, dst, recv, src):
+        m = min(send.shape[0], recv.shape[0])
+        if m:
+            recv[:m].copy_(send[:m])
+        return []
 
 
 class LocalLines(_Local, LinePartitionedPropagator):
@@ -141,6 +147,8 @@ def main():
     ap.add_argument("--ranks", default="all")
     ap.add_argument("--link-gbps", type=float, default=57.6,
                     help="per-peer xGMI rate each way (one link per GPU pair)")
+    ap.add_argument("--chunks", type=int, default=4,
+                    help="last-hop chunks (4 = the product's 1:3:3:1 split, else equal)")
     args = ap.parse_args()
     spec = graphs.SHAPES[args.shape]
     S = graphs.synthetic_graph(args.shape, seed=0)
@@ -159,7 +167,7 @@ def main():
             recs = []
             for p in sel:
                 if cand == "features":
-                    prop = LocalFeatures(csr, rank=p, world_size=P)
+                    prop = LocalFeatures(csr, rank=p, world_size=P, chunks=args.chunks)
                     bounds, B = feature_bounds(F, P)
                     wcols = B
                 else:
@@ -167,7 +175,7 @@ def main():
                     if W == 0:
                         break
                     shard = make_shard(S.row_ptr, S.col_idx, S.val, p, P, "cuda")
-                    prop = LocalLines(shard, csr=csr)
+                    prop = LocalLines(shard, csr=csr, chunks=args.chunks)
                     prop._tail_ld = (max(F - T, 1) + 31) // 32 * 32
                     wcols = W
                 prop._reset_marks()
@@ -184,7 +192,8 @@ def main():
                 dst = torch.empty(nb, device="cuda")
                 step1, ready1 = timeline(prop, X0, K, args.reps, copy=(src, dst))
                 del src, dst
-                chunks = row_chunks(n, prop.chunks)
+                chunks = replicated_chunks(n, REPLICATED_CHUNKS if prop.chunks == 4
+                                           else (1,) * prop.chunks)
                 gbytes = [(P - 1) * (r1 - r0) * wcols * 4 for r0, r1 in chunks]
                 # one chunk's unpack (the block-copy launch of P blocks)
                 r0, r1 = chunks[-1]

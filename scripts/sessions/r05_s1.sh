@@ -12,4 +12,6 @@ timeout -k 10 300 python scripts/pad_ab.py > gpurun_out/pad_ab.log 2>&1 || exit 
 timeout -k 10 600 python scripts/replicated_rehearsal.py > gpurun_out/replicated_rehearsal.log 2>&1 || exit $?
 
 timeout -k 10 200 python scripts/host_breakdown.py > gpurun_out/host_breakdown.log 2>&1
+
+timeout -k 10 200 python scripts/combo_ab.py --shape pubmed --configs "base:;r4:rows_per_wave=4;r4x:rows_per_wave=4,xcd_slices=1;r2:rows_per_wave=2;r2x:rows_per_wave=2,xcd_slices=1" > gpurun_out/combo_pubmed.log 2>&1
 echo done

@@ -416,36 +416,53 @@ __global__ __launch_bounds__(64 * NW) void linear_split_kernel(
         // 8 k of one class, split into its three pieces, stored side by side
         const auto wd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(W), 0,
                                                           (int)((int64_t)C * K * 4), 0x00020000);
-        const int full = (NT - 1) * 64, units = full + 4 * Cl + 1;
-        for (int idx = threadIdx.x; idx < NC * units; idx += 64 * NW) {
-            const int c = idx / units, w = idx - c * units;
-            int r = 0, kk = 0;
-            bool zero = false;
-            if (w < full) {
-                r = (w >> 6) * 16 + (w & 15);
-                kk = (w >> 4) & 3;
-            } else if (w < full + 4 * Cl) {
-                kk = (w - full) / Cl;
-                r = (NT - 1) * 16 + (w - full - kk * Cl);
-            } else {
-                zero = true;
-            }
-            const int k0 = c * 32 + 8 * kk;
-            float e[8];
+        // one unit = 8 k (a granule) of one class row, split into its three
+        // pieces and stored at its lane's place in the chunk's operand block;
+        // units run along W's rows, so a wave's loads read 2 KB of one row
+        // contiguously (in operand order the lanes read 64 different rows:
+        // ~10 us of scattered line requests per workgroup)
+        const int full = (NT - 1) * 64;
+        const int G = NC * 4;  // granules per class row
+        constexpr int FU = 4;  // units per thread per round, loads all issued first
+        for (int base = threadIdx.x; base < C * G; base += FU * 64 * NW) {
+            f4 e[FU][2];
+            int dsto[FU];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const float x = __builtin_bit_cast(
-                    float, __builtin_amdgcn_raw_buffer_load_b32(
-                               wd, zero ? 0u : (uint32_t)(r * K + k0 + q) * 4u, 0, 0));
-                e[q] = (!zero && k0 + q < K) ? x : 0.0f;
-            }
-            uint32_t h[4], m[4], l[4];
+            for (int f = 0; f < FU; ++f) {
+                const int idx = base + f * 64 * NW;
+                const bool in = idx < C * G;
+                const int r = in ? idx / G : 0, g = in ? idx - r * G : 0;
+                const int c = g >> 2, kk = g & 3, n = r >> 4, jj = r & 15;
+                const int w = n < NT - 1 ? n * 64 + jj + 16 * kk : full + kk * Cl + jj;
+                dsto[f] = in ? c * cstride + w * 48 : -1;
+                const uint32_t off = (uint32_t)(r * K + 8 * g) * 4u;
+                e[f][0] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wd, off, 0, 0));
+                e[f][1] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(wd, off + 16, 0, 0));
+                if (8 * g + 8 > K) {  // the row's last granule: k >= K is the next row
 #pragma unroll
-            for (int p = 0; p < 4; ++p) split3(e[2 * p], e[2 * p + 1], h[p], m[p], l[p]);
-            char *dst = lds + c * cstride + w * 48;
-            *reinterpret_cast<u32x4 *>(dst) = u32x4{h[0], h[1], h[2], h[3]};
-            *reinterpret_cast<u32x4 *>(dst + 16) = u32x4{m[0], m[1], m[2], m[3]};
-            *reinterpret_cast<u32x4 *>(dst + 32) = u32x4{l[0], l[1], l[2], l[3]};
+                    for (int q = 0; q < 8; ++q)
+                        if (8 * g + q >= K) e[f][q >> 2][q & 3] = 0.0f;
+                }
+            }
+#pragma unroll
+            for (int f = 0; f < FU; ++f) {
+                uint32_t h[4], m[4], l[4];
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+                    split3(e[f][p >> 1][2 * (p & 1)], e[f][p >> 1][2 * (p & 1) + 1], h[p], m[p], l[p]);
+                if (dsto[f] >= 0) {
+                    char *dst = lds + dsto[f];
+                    *reinterpret_cast<u32x4 *>(dst) = u32x4{h[0], h[1], h[2], h[3]};
+                    *reinterpret_cast<u32x4 *>(dst + 16) = u32x4{m[0], m[1], m[2], m[3]};
+                    *reinterpret_cast<u32x4 *>(dst + 32) = u32x4{l[0], l[1], l[2], l[3]};
+                }
+            }
+        }
+        // the zero granule of each chunk's last class tile (its lanes past Cl)
+        for (int c = threadIdx.x; c < NC; c += 64 * NW) {
+            char *dst = lds + c * cstride + (full + 4 * Cl) * 48;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4 *>(dst + 16 * p) = u32x4{0u, 0u, 0u, 0u};
         }
     }
     __syncthreads();

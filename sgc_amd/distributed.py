@@ -1117,6 +1117,66 @@ def _copy_blocks(src, dst, segs):
                                            _lib.stream_handle(src.device)), "copy_blocks_f32")
 
 
+# Row fractions of the replicated output's last-hop chunks: a small first
+# chunk (its all-gather starts as early as possible: at P = 8 the link time,
+# not the hop, is the critical path), two large ones, a small last one (the
+# last gather and unpack after the hop are short).
+REPLICATED_CHUNKS = (1, 3, 3, 1)
+
+
+def replicated_chunks(n, fractions=REPLICATED_CHUNKS):
+    """[(r0, r1)] row ranges covering [0, n) in proportion to `fractions`
+    (empty ranges dropped)."""
+    tot = sum(fractions)
+    cuts, acc = [0], 0
+    for f in fractions:
+        acc += f
+        cuts.append(n * acc // tot)
+    return [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a] or [(0, n)]
+
+
+def _replicated_last_hop(prop, n, P, p, ld, X0, hop_into, gather, unpack):
+    """The replicated output's last hop (feature and line partitions): in row
+    chunks (replicated_chunks), each computed into this rank's slot of its
+    chunk's [P*rows, ld] gather buffer and all-gathered in place as soon as it
+    is done; on the GPU the chunks alternate between two streams, so a chunk's
+    launch does not wait for the previous chunk's hub rows to join (each
+    gather is issued from its chunk's stream and waits for exactly that
+    chunk).  The caller's stream then waits for each gather and unpacks that
+    chunk into X_K (one block-copy launch).
+    hop_into(r0, r1, loc) computes rows [r0, r1) into loc; gather(full, loc)
+    returns a work handle (or None: done on the current stream); unpack(full,
+    r0, r1) lands the gathered chunk."""
+    gpu = X0.is_cuda
+    if gpu:
+        cur = torch.cuda.current_stream(X0.device)
+        if getattr(prop, "_chunk_streams", None) is None or \
+                prop._chunk_streams[0].device != X0.device:
+            prop._chunk_streams = [torch.cuda.Stream(X0.device) for _ in range(2)]
+    pending = []
+    chunks = replicated_chunks(n, REPLICATED_CHUNKS if prop.chunks == 4 else (1,) * prop.chunks)
+    for ci, (r0, r1) in enumerate(chunks):
+        rows = r1 - r0
+        full = prop._buf(("full", ci), (P * rows, ld), X0)
+        loc = _gather_slot(full, p, rows)  # in-place gather: no copy of our block
+        if gpu:
+            st = prop._chunk_streams[ci % 2]
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                hop_into(r0, r1, loc)
+                work = gather(full, loc)
+                if work is None:
+                    work = _StreamDone(st)
+        else:
+            hop_into(r0, r1, loc)
+            work = gather(full, loc)
+        pending.append((r0, r1, full, work))
+    for r0, r1, full, work in pending:
+        if work is not None:
+            work.wait()  # the caller's stream waits for this chunk's gather
+        unpack(full, r0, r1)
+
+
 def _gather_slot(full, p, rows):
     """Rank p's slot of an all-gather buffer [P*rows, ld]: the last hop writes
     its rows there and the gather runs in place (NCCL/RCCL in-place
@@ -1359,22 +1419,16 @@ class FeaturePartitionedPropagator:
         # last hop in row chunks, each computed into this rank's slot of the
         # chunk's gather buffer and gathered in place as soon as it is done;
         # every gathered chunk then lands in X_K's columns in one launch
-        pending = []
-        for ci, (r0, r1) in enumerate(row_chunks(n, self.chunks)):
-            rows = r1 - r0
-            if not rows:
-                continue
-            full = self._buf(("full", ci), (P * rows, B), X0)
-            loc = _gather_slot(full, p, rows)
+
+        def hop_into(r0, r1, loc):
             if w:
                 hop(src, r0, r1, loc[:, :w], own, True)
-            pending.append((r0, r1, full, self._all_gather(full, loc)))
-        for r0, r1, full, work in pending:
-            if work is not None:
-                work.wait()  # the compute stream waits for this chunk's gather
+
+        def unpack(full, r0, r1):
             rows = r1 - r0
             _copy_blocks(full, out, [(q * rows, 0, r0, int(bounds[q]), rows,
                                       int(bounds[q + 1] - bounds[q])) for q in range(P)])
+        _replicated_last_hop(self, n, P, p, B, X0, hop_into, self._all_gather, unpack)
         return out
 
 
@@ -1587,23 +1641,16 @@ class LinePartitionedPropagator:
             return
         if W == 0:  # all-tail layout (F < 32 P): no main blocks to exchange (W is
             return  # the same on every rank, so every rank skips the same calls)
-        p = self.rank
-        pending = []
-        for ci, (r0, r1) in enumerate(row_chunks(n, self.chunks)):
-            rows = r1 - r0
-            if not rows:
-                continue
-            full = self._buf(("full", ci), (P * rows, ld), X0)
-            loc = _gather_slot(full, p, rows)  # in-place gather: no copy of our block
+        def hop_into(r0, r1, loc):
             if w:
                 main_hop(msrc, r0, r1, loc[:, :w], mown, True)
-            pending.append((r0, r1, full, self._collective("gather", full, loc)))
-        for r0, r1, full, work in pending:
-            if work is not None:
-                work.wait()
+
+        def unpack(full, r0, r1):
             rows = r1 - r0
             _copy_blocks(full, out, [(q * rows, 0, r0, min(q * W, F), rows,
                                       min((q + 1) * W, F) - min(q * W, F)) for q in range(P)])
+        _replicated_last_hop(self, n, P, self.rank, ld, X0, hop_into,
+                             lambda full, loc: self._collective("gather", full, loc), unpack)
 
     def _last_sharded(self, msrc, mown, out, main_hop, W, w, rb, P, X0):
         n = msrc.shape[0]
