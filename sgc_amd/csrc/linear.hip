@@ -348,6 +348,7 @@ __host__ __device__ constexpr int split_chunk_bytes(int NT, int Cl) {
     return (NT - 1) * 3072 + (4 * Cl + 1) * 48;
 }
 
+
 // DIAG (diagnostics, sgc_set_tuning("linear_kernel", 6 / 7 / 8)): 1 = the
 // loads, the exchange and the stores without the split and the MFMAs; 2 = 1
 // without the stores; 3 = everything but the stores.
@@ -423,7 +424,7 @@ __global__ __launch_bounds__(64 * NW) void linear_split_kernel(
         // ~10 us of scattered line requests per workgroup)
         const int full = (NT - 1) * 64;
         const int G = NC * 4;  // granules per class row
-        constexpr int FU = 4;  // units per thread per round, loads all issued first
+        constexpr int FU = 8;  // units per thread per round, loads all issued first
         for (int base = threadIdx.x; base < C * G; base += FU * 64 * NW) {
             f4 e[FU][2];
             int dsto[FU];
@@ -482,7 +483,8 @@ __global__ __launch_bounds__(64 * NW) void linear_split_kernel(
         }
     const auto yd = __builtin_amdgcn_make_buffer_rsrc(Y, 0, (int)((int64_t)M * ldy * 4),
                                                       0x00020000);  // < 2^31
-    constexpr int PT = NT <= 2 ? kSplitHeld + 2 : NT == 3 ? kSplitHeld : kSplitHeld - 2;
+    constexpr int PT0 = NT <= 2 ? kSplitHeld + 2 : NT == 3 ? kSplitHeld : kSplitHeld - 2;
+    constexpr int PT = PT0 < 1 ? 1 : PT0;
     f4 held[PT][NT];
     uint32_t hrow[PT];
     int nheld = 0;  // uniform
@@ -497,17 +499,17 @@ __global__ __launch_bounds__(64 * NW) void linear_split_kernel(
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o[n]), yd,
                                                    cl0 + 4 <= C ? yrow + 4u * cl0 : kOffOOB, 0, 0);
         }
-        if (C < NT * 16) {  // uniform: a partial last class tile
+        // the partial group of four (only one lane group has one: C % 4 classes)
+        if (C % 4) {  // uniform
             // (the elements as separate values first: extracting them from
             // the vector the b128 store took was miscompiled -- every b32
             // store wrote element 0)
             const u32x4 pe = __builtin_bit_cast(u32x4, o[NT - 1]);
-            const uint32_t e0 = pe.x, e1 = pe.y, e2 = pe.z, e3 = pe.w;
+            const uint32_t e0 = pe.x, e1 = pe.y, e2 = pe.z;
             auto off = [&](int r) { return (ppart && pcl + r < C) ? yrow + 4u * (pcl + r) : kOffOOB; };
             __builtin_amdgcn_raw_buffer_store_b32(e0, yd, off(0), 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(e1, yd, off(1), 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(e2, yd, off(2), 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(e3, yd, off(3), 0, 0);
+            if (C % 4 >= 2) __builtin_amdgcn_raw_buffer_store_b32(e1, yd, off(1), 0, 0);
+            if (C % 4 == 3) __builtin_amdgcn_raw_buffer_store_b32(e2, yd, off(2), 0, 0);
         }
     };
     auto flush = [&]() {
