@@ -5,7 +5,9 @@ Used by bench.py (its `classifier` sub-record) and runnable on its own:
 
     python -m sgc_amd.classifier_bench [--rows 152410] [--features 602] [--classes 41]
 
-Times, with events on the current stream, medians over --reps:
+Times, with events on the current stream, medians over --reps (forward and
+backward: per call over 10 back-to-back calls, the kernels' own time; the
+single-call figure, launch gap included, beside it):
   forward       SGC.forward on ROCm = sgc_linear_f32 (fp32 MFMA), and torch's
                 F.linear beside it;
   backward      the weight gradients of the forward (sgc_linear_backward_f32:
@@ -32,7 +34,10 @@ from torch import optim
 HBM_PEAK_GBS = 8000.0
 
 
-def _median_ms(fn, reps, warmup=3):
+def _median_ms(fn, reps, warmup=3, inner=1):
+    """Median over `reps` event pairs of the time per call, each pair around
+    `inner` back-to-back calls (inner > 1: the launch gap between calls is
+    hidden, so the figure is the kernels' own time, as rocprofv3 reports it)."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -40,10 +45,11 @@ def _median_ms(fn, reps, warmup=3):
     for _ in range(reps):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        fn()
+        for _ in range(inner):
+            fn()
         e.record()
         torch.cuda.synchronize()
-        ms.append(s.elapsed_time(e))
+        ms.append(s.elapsed_time(e) / inner)
     return float(np.median(ms))
 
 
@@ -87,19 +93,22 @@ def classifier_record(dev, M=152410, K=602, C=41, reps=20, epochs=2, seed=0):
            "what": "Reddit-train shape (reddit.py:45-49 train rows, models.py:7-18)"}
     fwd_bytes = 4 * M * K + 4 * M * C + 4 * C * K
     bwd_bytes = 4 * M * K + 4 * M * C
-    t = _median_ms(lambda: linear(x, W, b), reps)
+    t = _median_ms(lambda: linear(x, W, b), reps, inner=10)
+    t1 = _median_ms(lambda: linear(x, W, b), reps)
     from . import _lib
     kname = _lib.load().sgc_linear_kernel_name(M, K, x.stride(0), C, _lib.ptr(x)).decode()
     rec["forward"] = {"kernel": f"{kname} (sgc_linear_f32; name from sgc_linear_kernel_name)",
-                      "ms": t,
+                      "ms": t, "single_call_ms": t1,
                       "bytes": fwd_bytes, "achieved_GBps": fwd_bytes / t / 1e6,
                       "frac": fwd_bytes / t / 1e6 / HBM_PEAK_GBS,
-                      "torch_F_linear_ms": _median_ms(lambda: F.linear(x, W, b), reps)}
-    t = _median_ms(lambda: linear_backward(x, dY), reps)
+                      "torch_F_linear_ms": _median_ms(lambda: F.linear(x, W, b), reps, inner=10)}
+    t = _median_ms(lambda: linear_backward(x, dY), reps, inner=10)
+    t1 = _median_ms(lambda: linear_backward(x, dY), reps)
     rec["backward"] = {"kernel": "xent_dw_kernel + reductions (sgc_linear_backward_f32)", "ms": t,
+                       "single_call_ms": t1,
                        "bytes": bwd_bytes, "achieved_GBps": bwd_bytes / t / 1e6,
                        "frac": bwd_bytes / t / 1e6 / HBM_PEAK_GBS,
-                       "torch_ms": _median_ms(lambda: (dY.t() @ x, dY.sum(0)), reps)}
+                       "torch_ms": _median_ms(lambda: (dY.t() @ x, dY.sum(0)), reps, inner=10)}
 
     def closure(m, fused=False):
         def run():
