@@ -18,10 +18,15 @@ Measured, per rank and candidate:
       sharded output (the difference is the replication's local work);
   chunk_ready_ms  when each last-hop chunk's rows are done (events), the run
       repeated with a concurrent copy of the gather's bytes on a second
-      stream ((P-1)/P of X_K read and written: the HBM traffic RCCL's
-      all-gather adds on a rank) -- the compute timeline under that
-      interference is the one the projection uses;
-  unpack_ms  one chunk's block-copy launch.
+      stream from the first chunk's readiness on ((P-1)/P of X_K read and
+      written: the HBM traffic RCCL's all-gathers add on a rank, here all at
+      HBM speed rather than spread over the link time) -- the compute
+      timeline under that interference is the one the projection uses;
+  unpack_ms  one chunk's block-copy launch;
+  breakdown (--breakdown)  the replicated step with the final unpacks
+      skipped, and with the last hop in one chunk (with and without the
+      unpacks): compute_replicated - compute_sharded split into the unpack,
+      the chunking and the rest.
 Modelled at a STATED link rate (one xGMI link per GPU pair, --link-gbps each
 way, a rank's ingress (P-1) links):
   chunk c's all-gather ((P-1) blocks of its rows) starts when the chunk is
@@ -53,12 +58,20 @@ class _Local:
     main-gather call records an event on the current stream: the moment its
     chunk's rows are done."""
 
+    side_copy = None  # (stream, src, dst): started at the first mark
+
     def _reset_marks(self):
         self.marks = []
 
     def _mark(self, dst):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
+        if not self.marks and self.side_copy is not None:
+            # the gathers' HBM traffic starts with the first gather
+            side, a, b = self.side_copy
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                b.copy_(a)
         self.marks.append((ev, dst.shape[0]))
 
 
@@ -110,26 +123,55 @@ def timeit(fn, reps, warm=2):
 
 def timeline(prop, X0, K, reps, copy=None):
     """Median (step ms, [chunk ready ms]) of the replicated step; `copy` =
-    (src, dst) copied on a second stream from the step's start."""
+    (src, dst) copied on a second stream from the moment the first chunk is
+    ready (when the first gather, and with it RCCL's traffic, starts)."""
     side = torch.cuda.Stream()
     steps, readies = [], []
+    prop.side_copy = None if copy is None else (side, copy[0], copy[1])
     for r in range(reps + 1):
         prop._reset_marks()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         s.record()
-        if copy is not None:
-            side.wait_event(s)
-            with torch.cuda.stream(side):
-                copy[1].copy_(copy[0])
         prop.propagate(X0, K, output="replicated")
         e.record()
+        torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         if r == 0:
             continue  # warm-up
         steps.append(s.elapsed_time(e))
         readies.append([s.elapsed_time(ev) for ev, _ in prop.marks])
+    prop.side_copy = None
     return float(np.median(steps)), [float(v) for v in np.median(np.array(readies), axis=0)]
+
+
+def breakdown(prop, X0, K, reps):
+    """The replicated step (a) with the unpacks of the gather buffers into
+    X_K skipped, (b) with the last hop in one chunk, (c) both."""
+    import sgc_amd.distributed as D
+    real = D._copy_blocks
+    fulls = {b.data_ptr() for k, b in prop._bufs.items() if k[0] == "full"}
+
+    def no_unpack(src, dst, segs):
+        if src.data_ptr() not in fulls:
+            real(src, dst, segs)
+
+    run = lambda: prop.propagate(X0, K, output="replicated")  # noqa: E731
+    res = {}
+    chunks = prop.chunks
+    for name, c, skip in (("no_unpack", chunks, True), ("one_chunk", 1, False),
+                          ("one_chunk_no_unpack", 1, True)):
+        prop.chunks = c
+        D._copy_blocks = no_unpack if skip else real
+        try:
+            run()
+            torch.cuda.synchronize()
+            fulls |= {b.data_ptr() for k, b in prop._bufs.items() if k[0] == "full"}
+            res[name] = timeit(run, reps)
+        finally:
+            D._copy_blocks = real
+            prop.chunks = chunks
+    return res
 
 
 def project(step_ms, ready_ms, gather_bytes, unpack_ms, ingress):
@@ -147,6 +189,12 @@ def main():
     ap.add_argument("--ranks", default="all")
     ap.add_argument("--link-gbps", type=float, default=57.6,
                     help="per-peer xGMI rate each way (one link per GPU pair)")
+    ap.add_argument("--schedules", default="",
+                    help="';'-separated knob sets of the last hop's chunk schedule, e.g. "
+                         "'alone=0,hub=0;alone=1,hub=1' (sgc_amd.distributed "
+                         "FIRST_CHUNK_ALONE / HUB_EARLY); default: the product's")
+    ap.add_argument("--breakdown", action="store_true",
+                    help="time the replicated step without unpacks / in one chunk too")
     ap.add_argument("--chunks", type=int, default=4,
                     help="last-hop chunks (4 = the product's 1:3:3:1 split, else equal)")
     args = ap.parse_args()
@@ -158,6 +206,17 @@ def main():
     out = torch.empty((n, F), device="cuda")
     t1 = timeit(lambda: propagate(csr, X0, K, out=out), args.reps)
     print(json.dumps({"case": "single", "shape": args.shape, "ms": t1}), flush=True)
+    import sgc_amd.distributed as D
+    scheds = [dict(kv.split("=") for kv in part.split(",") if kv)
+              for part in args.schedules.split(";")] if args.schedules else [{}]
+    for sched in scheds:
+        D.FIRST_CHUNK_ALONE = bool(int(sched.get("alone", int(D.FIRST_CHUNK_ALONE))))
+        D.HUB_EARLY = bool(int(sched.get("hub", int(D.HUB_EARLY))))
+        run_schedule(args, S, csr, X0, out, t1, F, K, n,
+                     {"alone": int(D.FIRST_CHUNK_ALONE), "hub": int(D.HUB_EARLY)})
+
+
+def run_schedule(args, S, csr, X0, out, t1, F, K, n, sched):
     for P in (int(v) for v in args.P.split(",")):
         ingress = (P - 1) * args.link_gbps * 1e9
         best = {"replicate": t1}
@@ -209,7 +268,8 @@ def main():
                     tb = (P - 1) * shard.block * prop._tail_ld * 4
                     tail_exposed = K * max(0.0, tb / ingress * 1e3 - step0 / (K + 1))
                 proj = project(step1, ready1, gbytes, t_unpack, ingress) + tail_exposed
-                rec = {"case": "rank", "P": P, "candidate": cand, "rank": p,
+                bd = breakdown(prop, X0, K, args.reps) if args.breakdown else None
+                rec = {"case": "rank", "schedule": sched, "P": P, "candidate": cand, "rank": p,
                        "block_cols": wcols, "compute_replicated_ms": t_rep,
                        "compute_sharded_ms": t_sh, "replication_local_ms": t_rep - t_sh,
                        "step_ms": step0, "chunk_ready_ms": ready0,
@@ -218,6 +278,8 @@ def main():
                        "gather_ms": [v / ingress * 1e3 for v in gbytes],
                        "unpack_ms": t_unpack, "tail_exposed_ms": tail_exposed,
                        "projected_replicated_ms": proj}
+                if bd is not None:
+                    rec["breakdown_ms"] = dict(bd, sharded=t_sh, replicated=t_rep)
                 print(json.dumps(rec), flush=True)
                 recs.append(rec)
                 del prop
@@ -226,7 +288,7 @@ def main():
                 best[cand] = max(r["projected_replicated_ms"] for r in recs)
                 rank_recs[cand] = recs
         chosen = min(best, key=best.get)
-        summ = {"case": "summary", "P": P, "single_ms": t1, "link_GBps_each_way": args.link_gbps,
+        summ = {"case": "summary", "schedule": sched, "P": P, "single_ms": t1, "link_GBps_each_way": args.link_gbps,
                 "projected_ms": best, "projected_speedup": {c: t1 / v for c, v in best.items()},
                 "auto_would_choose": chosen, "auto_speedup": t1 / best[chosen],
                 "replication_local_ms_max": {c: max(r["replication_local_ms"] for r in rs)

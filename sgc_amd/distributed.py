@@ -1157,27 +1157,57 @@ def _chunk_order(csr, chunks):
     return order
 
 
+# Schedule of the replicated last hop's chunks (A/B knobs of
+# scripts/replicated_rehearsal.py; results never depend on them):
+#  FIRST_CHUNK_ALONE  the other chunks start after the first one, so its
+#                     gather (the link's first work) is not slowed by the
+#                     chunk beside it;
+#  HUB_EARLY          the hub rows of the chunk holding the longest row run
+#                     first, on a stream of their own, the rest of that chunk
+#                     in its turn -- its serial chain no longer starts only
+#                     when the chunks before it are done; off: the hub launch
+#                     delayed the first chunk by ~0.25 ms and every P=8
+#                     projection dropped (profiles/r05/rehearsal_sched.log).
+FIRST_CHUNK_ALONE = True
+HUB_EARLY = False
+
+
 def _replicated_last_hop(prop, n, P, p, ld, X0, hop_into, gather, unpack):
     """The replicated output's last hop (feature and line partitions): in row
     chunks (replicated_chunks), each computed into this rank's slot of its
     chunk's [P*rows, ld] gather buffer and all-gathered in place as soon as it
-    is done; on the GPU the chunks alternate between two streams, so a chunk's
-    launch does not wait for the previous chunk's hub rows to join (each
-    gather is issued from its chunk's stream and waits for exactly that
-    chunk).  The caller's stream then waits for each gather and unpacks that
+    is done; on the GPU the first chunk runs alone, the others alternate
+    between two streams (a chunk's launch does not wait for the previous
+    chunk's hub rows to join); with HUB_EARLY the hub rows of the chunk
+    holding the longest row (the last one, _chunk_order) start at once on a
+    third stream (measured slower: they delay the first chunk).
+    Each gather is issued from its chunk's stream and waits for exactly that
+    chunk.  The caller's stream then waits for each gather and unpacks that
     chunk into X_K (one block-copy launch).
-    hop_into(r0, r1, loc) computes rows [r0, r1) into loc; gather(full, loc)
-    returns a work handle (or None: done on the current stream); unpack(full,
-    r0, r1) lands the gathered chunk."""
+    hop_into(r0, r1, loc, flags=0) computes rows [r0, r1) into loc (flags:
+    SPMM_HUB_ONLY / SPMM_NO_HUB for the split hub chunk); gather(full, loc)
+    returns a work handle (or None: done on the current stream);
+    unpack(full, r0, r1) lands the gathered chunk."""
+    from .propagate import SPMM_HUB_ONLY, SPMM_NO_HUB
     gpu = X0.is_cuda
     if gpu:
         cur = torch.cuda.current_stream(X0.device)
         if getattr(prop, "_chunk_streams", None) is None or \
                 prop._chunk_streams[0].device != X0.device:
-            prop._chunk_streams = [torch.cuda.Stream(X0.device) for _ in range(2)]
+            prop._chunk_streams = [torch.cuda.Stream(X0.device) for _ in range(3)]
     pending = []
     chunks = replicated_chunks(n, REPLICATED_CHUNKS if prop.chunks == 4 else (1,) * prop.chunks)
-    for i, ci in enumerate(_chunk_order(getattr(prop, "csr", None), chunks)):
+    order = _chunk_order(getattr(prop, "csr", None), chunks)
+    hub_split = gpu and HUB_EARLY and len(order) > 1
+    if hub_split:  # the hub chunk's hub rows first, beside everything else
+        sh = prop._chunk_streams[2]
+        sh.wait_stream(cur)
+        r0, r1 = chunks[order[-1]]
+        full = prop._buf(("full", order[-1]), (P * (r1 - r0), ld), X0)
+        with torch.cuda.stream(sh):
+            hop_into(r0, r1, _gather_slot(full, p, r1 - r0), SPMM_HUB_ONLY)
+    first_done = None
+    for i, ci in enumerate(order):
         r0, r1 = chunks[ci]
         rows = r1 - r0
         full = prop._buf(("full", ci), (P * rows, ld), X0)
@@ -1185,8 +1215,16 @@ def _replicated_last_hop(prop, n, P, p, ld, X0, hop_into, gather, unpack):
         if gpu:
             st = prop._chunk_streams[i % 2]
             st.wait_stream(cur)
+            if first_done is not None and i % 2:
+                st.wait_event(first_done)
+            split = hub_split and i == len(order) - 1
             with torch.cuda.stream(st):
-                hop_into(r0, r1, loc)
+                hop_into(r0, r1, loc, SPMM_NO_HUB if split else 0)
+                if i == 0 and FIRST_CHUNK_ALONE:
+                    first_done = torch.cuda.Event()
+                    first_done.record(st)
+                if split:
+                    st.wait_stream(prop._chunk_streams[2])
                 work = gather(full, loc)
                 if work is None:
                     work = _StreamDone(st)
@@ -1390,12 +1428,13 @@ class FeaturePartitionedPropagator:
             out = torch.empty(shape, dtype=torch.float32, device=X0.device)
         from .propagate import SPMM_X_PADDED, SPMM_Y_PADDED
 
-        def hop(src, r0, r1, dst, own_src, own_dst):
+        def hop(src, r0, r1, dst, own_src, own_dst, flags=0):
             # own buffers: 4-float pad columns may be read / written (16-B
             # lanes at any block width); results never depend on it
             if self._padded_ok:
-                fl = (SPMM_X_PADDED if own_src else 0) | (SPMM_Y_PADDED if own_dst else 0)
-                return self.spmm_fn(src, r0, r1, dst, flags=fl)
+                flags |= (SPMM_X_PADDED if own_src else 0) | (SPMM_Y_PADDED if own_dst else 0)
+            if flags:
+                return self.spmm_fn(src, r0, r1, dst, flags=flags)
             return self.spmm_fn(src, r0, r1, dst)
 
         # hop 1 reads the caller's block in place when its rows are 16-B
@@ -1443,9 +1482,9 @@ class FeaturePartitionedPropagator:
         # chunk's gather buffer and gathered in place as soon as it is done;
         # every gathered chunk then lands in X_K's columns in one launch
 
-        def hop_into(r0, r1, loc):
+        def hop_into(r0, r1, loc, flags=0):
             if w:
-                hop(src, r0, r1, loc[:, :w], own, True)
+                hop(src, r0, r1, loc[:, :w], own, True, flags)
 
         def unpack(full, r0, r1):
             rows = r1 - r0
@@ -1590,10 +1629,11 @@ class LinePartitionedPropagator:
             out = torch.empty(shape, dtype=torch.float32, device=X0.device)
         from .propagate import SPMM_X_PADDED, SPMM_Y_PADDED
 
-        def main_hop(src, r0, r1, dst, own_src, own_dst):
+        def main_hop(src, r0, r1, dst, own_src, own_dst, flags=0):
             if self._padded_ok:
-                fl = (SPMM_X_PADDED if own_src else 0) | (SPMM_Y_PADDED if own_dst else 0)
-                return self.main_spmm_fn(src, r0, r1, dst, flags=fl)
+                flags |= (SPMM_X_PADDED if own_src else 0) | (SPMM_Y_PADDED if own_dst else 0)
+            if flags:
+                return self.main_spmm_fn(src, r0, r1, dst, flags=flags)
             return self.main_spmm_fn(src, r0, r1, dst)
 
         def aligned(v, col0, width):  # 16-B lanes readable in place
@@ -1665,9 +1705,9 @@ class LinePartitionedPropagator:
             return
         if W == 0:  # all-tail layout (F < 32 P): no main blocks to exchange (W is
             return  # the same on every rank, so every rank skips the same calls)
-        def hop_into(r0, r1, loc):
+        def hop_into(r0, r1, loc, flags=0):
             if w:
-                main_hop(msrc, r0, r1, loc[:, :w], mown, True)
+                main_hop(msrc, r0, r1, loc[:, :w], mown, True, flags)
 
         def unpack(full, r0, r1):
             rows = r1 - r0
