@@ -327,6 +327,33 @@ int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd,
 int sgc_copy_blocks_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int32_t nseg,
                         const int64_t *segs_host, void *stream);
 
+/* Recorded launch lists: the K-hop loop's launches (sgc_spmm_csr_f32_ex /
+ * sgc_pad_rows_f32 with their arguments) recorded once and replayed by ONE
+ * call per propagation -- at Pubmed shape the per-launch host cost (~4 us)
+ * is a tenth of a hop.  A pointer argument of a recorded launch is either
+ * fixed (SGC_SLOT_FIXED: the recorded pointer, e.g. an intermediate buffer the
+ * caller keeps alive) or the run's X_0 / X_K (SGC_SLOT_X0 / SGC_SLOT_OUT: the
+ * pointers given to sgc_launch_list_run), so one list serves every feature
+ * tensor of the recorded shape, strides and alignment; each replayed launch
+ * makes its kernel choice from the actual pointers, as a direct call does.
+ * A list belongs to the device current at creation (the run switches to it
+ * and back).  Not for concurrent runs of one list on different streams when
+ * it holds fixed intermediates.  No reference counterpart: the reference's
+ * loop (utils.py:94-96) is one torch.spmm call per hop. */
+enum { SGC_SLOT_FIXED = 0, SGC_SLOT_X0 = 1, SGC_SLOT_OUT = 2 };
+int sgc_launch_list_create(int64_t *handle_host);
+int sgc_launch_list_add_spmm(int64_t handle, const int32_t *row_ptr, const int32_t *col_idx,
+                             const float *val, int64_t row_begin, int64_t row_end,
+                             const float *X, int64_t ldx, float *Y, int64_t ldy, int64_t F,
+                             const int32_t *plan, int64_t n_heavy, int64_t n_hub,
+                             int32_t heavy_threshold, uint32_t flags, int32_t x_slot,
+                             int32_t y_slot);
+int sgc_launch_list_add_pad_rows(int64_t handle, const float *src, int64_t lds, float *dst,
+                                 int64_t ldd, int64_t n_rows, int64_t F, int32_t src_slot,
+                                 int32_t dst_slot);
+int sgc_launch_list_run(int64_t handle, const float *X0, float *out, void *stream);
+int sgc_launch_list_destroy(int64_t handle);
+
 /* The row stride (floats) the engine uses for its own feature buffers. */
 int64_t sgc_aligned_ld(int64_t F);
 

@@ -5,8 +5,10 @@
 Medians (us) of each piece of the call's host path, timed on its own:
 the whole synchronised call, torch.cuda.synchronize() when idle, csr_of, the
 multi-GPU checks (process_group, devices_from_env), check_propagation_inputs,
-the result's allocation, propagate()'s enqueue (prepared loop), one
-sgc_spmm_csr_f32_ex launch, and the GPU time of the hops (events).
+the result's allocation, propagate()'s enqueue (prepared loop), the
+recorded launch list replayed bare (one sgc_launch_list_run call), the GPU
+time of the hops (events), and each enqueue followed by a device or stream
+synchronise.
 """
 import argparse
 import json
@@ -19,7 +21,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from sgc_amd import graphs, multigpu  # noqa: E402
+from sgc_amd import _lib, graphs, multigpu  # noqa: E402
 from sgc_amd.propagate import check_propagation_inputs, csr_of, propagate  # noqa: E402
 from sgc_amd.utils import sgc_precompute  # noqa: E402
 
@@ -54,6 +56,10 @@ def main():
     rec = {"shape": a.shape, "K": K}
     rec["call_us"] = med(lambda: sgc_precompute(X, adj, K), a.reps)
     rec["sync_idle_us"] = med(torch.cuda.synchronize, a.reps)
+    rec["sync_dev_arg_idle_us"] = med(lambda: torch.cuda.synchronize(dev), a.reps)
+    rec["current_device_us"] = med(torch.cuda.current_device, a.reps)
+    rec["stream_handle_us"] = med(lambda: _lib.stream_handle(dev), a.reps)
+    rec["capturing_us"] = med(torch.cuda.is_current_stream_capturing, a.reps)
     rec["csr_of_us"] = med(lambda: csr_of(adj), a.reps)
     rec["process_group_us"] = med(lambda: multigpu.process_group(dev), a.reps)
     rec["devices_from_env_us"] = med(lambda: multigpu.devices_from_env(0), a.reps)
@@ -76,6 +82,24 @@ def main():
         ev.append((s, e))
     torch.cuda.synchronize()
     rec["gpu_events_us"] = float(np.median([s.elapsed_time(e) for s, e in ev])) * 1e3
+    # the synchronised pieces: enqueue + wait, with the device-wide and the
+    # stream's synchronise, and the prepared launches replayed bare
+    cs = torch.cuda.current_stream(dev)
+    rec["propagate_devsync_us"] = med(lambda: (propagate(csr, X, K, out=out),
+                                               torch.cuda.synchronize()), a.reps)
+    rec["propagate_streamsync_us"] = med(lambda: (propagate(csr, X, K, out=out),
+                                                  cs.synchronize()), a.reps)
+    prep = [v for k, v in csr._plans.items() if isinstance(k, tuple) and k[:1] == ("list",)]
+    handle = prep[-1][1].handle
+    lib = _lib.load()
+    xp, op, sh = X.data_ptr(), out.data_ptr(), _lib.stream_handle(dev)
+
+    def bare():  # the recorded launch list alone (one ctypes call)
+        lib.sgc_launch_list_run(handle, xp, op, sh)
+    rec["bare_enqueue_us"] = med(bare, min(a.reps, 200))
+    torch.cuda.synchronize()
+    rec["bare_devsync_us"] = med(lambda: (bare(), torch.cuda.synchronize()), a.reps)
+    rec["trivial_ctypes_call_us"] = med(lambda: lib.sgc_get_tuning(b"slice_floats"), a.reps)
     print(json.dumps(rec), flush=True)
 
 

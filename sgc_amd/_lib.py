@@ -54,6 +54,13 @@ SIGNATURES = {
     "sgc_pad_rows_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i64, _p]),
     "sgc_copy_blocks_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i32, _p, _p]),
     "sgc_aligned_ld": (_i64, [_i64]),
+    "sgc_launch_list_create": (ctypes.c_int, [ctypes.POINTER(_i64)]),
+    "sgc_launch_list_add_spmm": (ctypes.c_int, [_i64, _p, _p, _p, _i64, _i64, _p, _i64, _p, _i64,
+                                                _i64, _p, _i64, _i64, _i32, _u32, _i32, _i32]),
+    "sgc_launch_list_add_pad_rows": (ctypes.c_int, [_i64, _p, _i64, _p, _i64, _i64, _i64, _i32,
+                                                    _i32]),
+    "sgc_launch_list_run": (ctypes.c_int, [_i64, _p, _p, _p]),
+    "sgc_launch_list_destroy": (ctypes.c_int, [_i64]),
     "sgc_linear_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "sgc_linear_kernel_name": (ctypes.c_char_p, [_i64, _i64, _i64, _i64, _p]),
     "sgc_linear_xent_workspace": (_i64, [_i64, _i64, _i64]),

@@ -1,5 +1,8 @@
 // capi.hip -- extern "C" entry points of libsgc_amd.so (include/sgc_amd.h).
 #include <cstdarg>
+#include <map>
+#include <mutex>
+#include <vector>
 #include <cstdio>
 
 #include "common.h"
@@ -242,6 +245,142 @@ int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int
 int sgc_copy_blocks_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int32_t nseg,
                         const int64_t *segs_host, void *stream) {
     return launch_copy_blocks(src, lds, dst, ldd, nseg, segs_host, as_stream(stream));
+}
+
+// Recorded launch lists (sgc_launch_list_*): the K-hop loop's launches built
+// once with their arguments, replayed by one call per propagation.  X_0 and
+// X_K enter by slot, so one list serves every feature tensor of the recorded
+// shape / strides / alignment on its stream.
+}  // extern "C"
+
+namespace sgc {
+namespace {
+
+struct ListOp {
+    int kind;  // 0 spmm (launch_spmm), 1 pad rows (launch_pad_rows)
+    const int32_t *row_ptr, *col_idx;
+    const float *val;
+    int64_t row_begin, row_end;
+    const float *X;
+    int64_t ldx;
+    float *Y;
+    int64_t ldy, F;
+    const int32_t *plan;
+    int64_t n_heavy, n_hub;
+    int32_t threshold;
+    uint32_t flags;
+    int32_t x_slot, y_slot;  // SGC_SLOT_*: the pointer as recorded, or the run's X_0 / X_K
+};
+
+struct LaunchList {
+    int device = 0;
+    std::vector<ListOp> ops;
+};
+
+std::mutex g_lists_mu;
+std::map<int64_t, LaunchList> g_lists;
+int64_t g_next_list = 1;
+
+template <typename T>
+T *slot_ptr(T *recorded, int32_t slot, const float *X, float *out) {
+    if (slot == SGC_SLOT_X0) return (T *)X;
+    if (slot == SGC_SLOT_OUT) return (T *)out;
+    return recorded;
+}
+
+}  // namespace
+}  // namespace sgc
+
+extern "C" {
+
+int sgc_launch_list_create(int64_t *handle_host) {
+    SGC_REQUIRE(handle_host, SGC_EINVAL, "launch_list_create: null handle");
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "launch_list_create: %s", hipGetErrorString(e));
+    std::lock_guard<std::mutex> lock(g_lists_mu);
+    const int64_t h = g_next_list++;
+    g_lists[h].device = dev;
+    *handle_host = h;
+    return SGC_OK;
+}
+
+int sgc_launch_list_destroy(int64_t handle) {
+    std::lock_guard<std::mutex> lock(g_lists_mu);
+    SGC_REQUIRE(g_lists.erase(handle) == 1, SGC_EINVAL, "launch_list_destroy: unknown handle %lld",
+                (long long)handle);
+    return SGC_OK;
+}
+
+static int list_add(int64_t handle, const ListOp &op) {
+    SGC_REQUIRE(op.x_slot >= SGC_SLOT_FIXED && op.x_slot <= SGC_SLOT_OUT && op.y_slot >= SGC_SLOT_FIXED &&
+                    op.y_slot <= SGC_SLOT_OUT,
+                SGC_EINVAL, "launch_list_add: bad slot (%d, %d)", op.x_slot, op.y_slot);
+    std::lock_guard<std::mutex> lock(g_lists_mu);
+    auto it = g_lists.find(handle);
+    SGC_REQUIRE(it != g_lists.end(), SGC_EINVAL, "launch_list_add: unknown handle %lld",
+                (long long)handle);
+    it->second.ops.push_back(op);
+    return SGC_OK;
+}
+
+int sgc_launch_list_add_spmm(int64_t handle, const int32_t *row_ptr, const int32_t *col_idx,
+                             const float *val, int64_t row_begin, int64_t row_end, const float *X,
+                             int64_t ldx, float *Y, int64_t ldy, int64_t F, const int32_t *plan,
+                             int64_t n_heavy, int64_t n_hub, int32_t heavy_threshold,
+                             uint32_t flags, int32_t x_slot, int32_t y_slot) {
+    constexpr uint32_t known = SGC_SPMM_X_PADDED | SGC_SPMM_Y_PADDED | SGC_SPMM_NO_HUB |
+                               SGC_SPMM_HUB_ONLY | SGC_SPMM_ACCUMULATE | SGC_SPMM_HUB_SERIAL |
+                               SGC_SPMM_LIGHT_ORDER | SGC_SPMM_X_UNDER_4G;
+    SGC_REQUIRE((flags & ~known) == 0, SGC_EINVAL, "launch_list_add_spmm: unknown flags 0x%x", flags);
+    SGC_REQUIRE(!((flags & SGC_SPMM_NO_HUB) && (flags & SGC_SPMM_HUB_ONLY)), SGC_EINVAL,
+                "launch_list_add_spmm: NO_HUB and HUB_ONLY together");
+    return list_add(handle, ListOp{0, row_ptr, col_idx, val, row_begin, row_end, X, ldx, Y, ldy, F,
+                                   plan, plan ? n_heavy : 0, plan ? n_hub : 0, heavy_threshold,
+                                   flags, x_slot, y_slot});
+}
+
+int sgc_launch_list_add_pad_rows(int64_t handle, const float *src, int64_t lds, float *dst,
+                                 int64_t ldd, int64_t n_rows, int64_t F, int32_t src_slot,
+                                 int32_t dst_slot) {
+    return list_add(handle, ListOp{1, nullptr, nullptr, nullptr, 0, n_rows, src, lds, dst, ldd, F,
+                                   nullptr, 0, 0, 0, 0u, src_slot, dst_slot});
+}
+
+int sgc_launch_list_run(int64_t handle, const float *X0, float *out, void *stream) {
+    const LaunchList *L = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(g_lists_mu);
+        auto it = g_lists.find(handle);
+        SGC_REQUIRE(it != g_lists.end(), SGC_EINVAL, "launch_list_run: unknown handle %lld",
+                    (long long)handle);
+        L = &it->second;  // map nodes are stable; a list is not destroyed while it runs
+    }
+    int cur = 0;
+    hipError_t e = hipGetDevice(&cur);
+    SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "launch_list_run: %s", hipGetErrorString(e));
+    if (cur != L->device) {
+        e = hipSetDevice(L->device);
+        SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "launch_list_run: %s", hipGetErrorString(e));
+    }
+    hipStream_t s = as_stream(stream);
+    int rc = SGC_OK;
+    for (const ListOp &op : L->ops) {
+        const float *x = slot_ptr(op.X, op.x_slot, X0, out);
+        float *y = slot_ptr(op.Y, op.y_slot, X0, out);
+        if (!x || !y) {
+            set_error("launch_list_run: null X_0 / X_K for a slot");
+            rc = SGC_EINVAL;
+            break;
+        }
+        rc = op.kind == 0 ? launch_spmm(op.row_ptr, op.col_idx, op.val, op.row_begin, op.row_end, x,
+                                        op.ldx, y, op.ldy, op.F, op.plan, op.n_heavy, op.n_hub,
+                                        op.threshold, op.flags, s)
+                          : launch_pad_rows(x, op.ldx, y, op.ldy, op.row_end, op.F, s);
+        if (rc != SGC_OK) break;
+    }
+    if (cur != L->device) (void)hipSetDevice(cur);
+    return rc;
 }
 
 int sgc_propagate_groups_f32(int32_t groups, const int32_t *row_ptrs, const int32_t *col_idx,

@@ -673,12 +673,13 @@ __device__ __forceinline__ void row_quadsT_pipe(const int *__restrict__ col,
 #ifndef SGC_HEAVY_VEC
 #define SGC_HEAVY_VEC 2
 #endif
-template <int HC, int NL>
+template <int HC, int NL, int IN>
 __device__ __forceinline__ void hub_body(
     int bid, const int *__restrict__ row_ptr, const int *__restrict__ col,
     const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
     float *__restrict__ Y, int64_t ldy, int row_begin, int F, const int *__restrict__ hub_rows,
     int n_chunks, int accum);
+constexpr int kFusedHubInstr = 8;  // (see HubShape)
 
 // HF > 0: the serial hub rows fused into the launch (as spmm_rows_kernel's HF).
 template <int V, int C, int U, int UH, int HF = 0>
@@ -694,7 +695,7 @@ __global__ __launch_bounds__(256) void spmm_csr_kernel(
     if constexpr (HF > 0) {
         if (bx < n_hub_blocks) {  // block-uniform
             if (blockIdx.y == 0)
-                hub_body<HF, 3>(bx, row_ptr, col, val, X, ldx, Y, ldy, row_begin, F, hub_rows,
+                hub_body<HF, 3, kFusedHubInstr>(bx, row_ptr, col, val, X, ldx, Y, ldy, row_begin, F, hub_rows,
                                 hub_chunks, accum);
             return;
         }
@@ -792,7 +793,7 @@ __global__ __launch_bounds__(256) void spmm_rows_kernel(
     if constexpr (HF > 0) {
         if (bx < n_hub_blocks) {  // block-uniform
             if (blockIdx.y == 0)
-                hub_body<HF, 3>(bx, row_ptr, col, val, X, ldx, Y, ldy, row_begin, F, hub_rows,
+                hub_body<HF, 3, kFusedHubInstr>(bx, row_ptr, col, val, X, ldx, Y, ldy, row_begin, F, hub_rows,
                                 hub_chunks, accum);
             return;
         }
@@ -1031,10 +1032,17 @@ constexpr int kHubDepth = 3;   // rounds held in loader registers (17 loads each
 constexpr int kHubUnroll = 6;  // lcm(kHubDepth, 2): X ring slot and colv parity compile-time
 constexpr int kHubPre = 4;     // LDS batches of 4 nonzeros the chain reads ahead
 
-template <int HC, int NL>
+// The fused rows + hub launches (hub_body<HF, 3> inside spmm_csr_kernel /
+// spmm_rows_kernel) stage IN = 8 nonzeros per loader lane: their LDS image is
+// 18 KB instead of 35 KB, and since every workgroup of a launch carries it,
+// eight workgroups (32 waves) fit a CU instead of four -- the light rows of a
+// small graph are latency-bound and need the occupancy (Pubmed shape: the
+// light rows alone ran 30.5 us per hop, fused at 35 KB 37.5 us).
+template <int HC, int NL, int IN = kHubInstr>
 struct HubShape {
+    static_assert(IN % 4 == 0 && IN <= kHubInstr, "loader run: whole b128 LDS writes");
     static constexpr int kSegs = kWave / HC;                     // nonzero runs per loader wave
-    static constexpr int kPerLoader = kHubInstr * kSegs;         // nonzeros per loader per round
+    static constexpr int kPerLoader = IN * kSegs;                // nonzeros per loader per round
     static constexpr int kRound = NL * kPerLoader;  // nonzeros per round (240 / 480 at NL = 15)
     static constexpr int kPad = 4 * kHubPre;        // read-ahead past kRound
     // dwords per gxT row: 4 mod 64 (conflict-free b128), and >= kRound + kPad
@@ -1208,13 +1216,13 @@ __device__ __forceinline__ void hub_chain_dpp(float &acc, uint32_t xa, uint32_t 
 // The body of one hub work item (hub row h, feature chunk c of block `bid`),
 // shared by spmm_hub_kernel and the fused rows + hub launch of
 // spmm_rows_kernel (HF > 0: NL = 3, the rows kernel's 256 threads).
-template <int HC, int NL>
+template <int HC, int NL, int IN>
 __device__ __forceinline__ void hub_body(
     int bid, const int *__restrict__ row_ptr, const int *__restrict__ col,
     const float *__restrict__ val, const float *__restrict__ X, int64_t ldx,
     float *__restrict__ Y, int64_t ldy, int row_begin, int F, const int *__restrict__ hub_rows,
     int n_chunks, int accum) {
-    using Sh = HubShape<HC, NL>;
+    using Sh = HubShape<HC, NL, IN>;
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) float gxT[2][HC * Sh::kStride];  // 2 x 66.5 KB
     __shared__ __attribute__((aligned(16)))
@@ -1229,14 +1237,14 @@ __device__ __forceinline__ void hub_body(
     const int row = hub_rows[h];
     const int k0 = row_ptr[row], k1 = row_ptr[row + 1];
     const int fl = lane & (HC - 1);  // feature within the chunk
-    const int seg = lane / HC;       // which run of kHubInstr nonzeros (HC = 32: 0 or 1)
+    const int seg = lane / HC;       // which run of IN nonzeros (HC = 32: 0 or 1)
     const int f = c * HC + fl;
     const uint32_t boff = (f < F ? (uint32_t)f : 0u) * 4u;
     const char *Xb = reinterpret_cast<const char *>(X);
     const int64_t row_bytes = ldx * 4;
     const int n_round = (k1 - k0 + Sh::kRound - 1) / Sh::kRound;
     const int my_k = lane & (Sh::kPerLoader - 1);  // this lane's nonzero of the loader's run
-    float regs[kHubDepth][kHubInstr];
+    float regs[kHubDepth][IN];
     float vreg[kHubDepth];
     int colv[2];  // column ids of the loader's run, one per lane, for two future rounds
     // Loader waves only; `s` and `p` are compile-time constants after unrolling.
@@ -1251,10 +1259,10 @@ __device__ __forceinline__ void hub_body(
     auto load_x = [&](int r, int s, int p) {
         const int kr = k0 + r * Sh::kRound + li * Sh::kPerLoader;
 #pragma unroll
-        for (int j = 0; j < kHubInstr; ++j) {
+        for (int j = 0; j < IN; ++j) {
             int cj = __builtin_amdgcn_readlane(colv[p], j);
             if (HC == 32) {
-                const int c1 = __builtin_amdgcn_readlane(colv[p], kHubInstr + j);
+                const int c1 = __builtin_amdgcn_readlane(colv[p], IN + j);
                 cj = seg ? c1 : cj;
             }
             regs[s][j] = *reinterpret_cast<const float *>(Xb + (int64_t)cj * row_bytes + boff);
@@ -1263,9 +1271,9 @@ __device__ __forceinline__ void hub_body(
     };
     auto store = [&](int buf, int s) {
         f4 *dst = reinterpret_cast<f4 *>(
-            &gxT[buf][fl * Sh::kStride + li * Sh::kPerLoader + seg * kHubInstr]);
+            &gxT[buf][fl * Sh::kStride + li * Sh::kPerLoader + seg * IN]);
 #pragma unroll
-        for (int q = 0; q < kHubInstr / 4; ++q)
+        for (int q = 0; q < IN / 4; ++q)
             dst[q] = f4{regs[s][4 * q], regs[s][4 * q + 1], regs[s][4 * q + 2], regs[s][4 * q + 3]};
         if (lane < Sh::kPerLoader) gv[buf][li * Sh::kPerLoader + lane] = vreg[s];
     };
@@ -1347,8 +1355,8 @@ __global__ __launch_bounds__(64 * (NL + 1)) void spmm_hub_kernel(
     const int *__restrict__ row_ptr, const int *__restrict__ col, const float *__restrict__ val,
     const float *__restrict__ X, int64_t ldx, float *__restrict__ Y, int64_t ldy, int row_begin,
     int F, const int *__restrict__ hub_rows, int n_chunks, int accum) {
-    hub_body<HC, NL>((int)blockIdx.x, row_ptr, col, val, X, ldx, Y, ldy, row_begin, F, hub_rows,
-                     n_chunks, accum);
+    hub_body<HC, NL, kHubInstr>((int)blockIdx.x, row_ptr, col, val, X, ldx, Y, ldy, row_begin, F,
+                                hub_rows, n_chunks, accum);
 }
 
 namespace {

@@ -74,6 +74,7 @@ class Plan(NamedTuple):
 
 NO_PLAN = Plan(None, 0, 0, 0)
 
+SLOT_FIXED, SLOT_X0, SLOT_OUT = 0, 1, 2  # sgc_launch_list_* pointer slots
 SPMM_X_PADDED = 1  # sgc_spmm_csr_f32_ex flags (include/sgc_amd.h)
 SPMM_Y_PADDED = 2
 SPMM_NO_HUB = 4    # split launch: every row but the plan's hub rows
@@ -234,10 +235,11 @@ class DeviceCSR:
         return self._plans[key]
 
     def release_prepared(self):
-        """Free propagate()'s prepared loops on this adjacency (each keeps its
-        launch arguments and up to PREPARED_LOOP_MAX_BYTES of intermediates;
-        at most PREPARED_LOOPS_KEPT of them).  The next call prepares again."""
-        for key in [k for k in self._plans if isinstance(k, tuple) and k[:1] == ("loop",)]:
+        """Free propagate()'s recorded launch lists on this adjacency (each
+        keeps its launches' arguments and up to PREPARED_LOOP_MAX_BYTES of
+        intermediates; at most PREPARED_LOOPS_KEPT of them).  The next call
+        records again."""
+        for key in [k for k in self._plans if isinstance(k, tuple) and k[:1] == ("list",)]:
             del self._plans[key]
 
     def drop_groups(self):
@@ -638,23 +640,23 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
                                              _lib.ptr(out), out.stride(0), F, int(K), _lib.ptr(ws),
                                              ws_bytes, cpu_threads()), "propagate_f32_cpu")
         return out
-    stream = _lib.stream_handle(X.device)
+    stream = torch.cuda.current_stream(X.device).cuda_stream  # (an int: ctypes takes it as void *)
     G_rule = column_groups_for(csr, F) if use_plan else 1
     # small launches (Cora / Pubmed shape: 20-40 us hops) pay their host time:
-    # the Python loop's ctypes calls are prepared once per (X, out, K, stream,
-    # schedule) and replayed, with the intermediates kept with them
+    # the loop's launches are recorded once per (shape, strides, X_0's 128-B
+    # alignment, K, stream, schedule) into a native launch list, with the
+    # intermediates kept beside it, and replayed by one call that takes this
+    # call's X_0 and X_K
     key = None
-    if (not native_loop and hop_hook is None and prepare and
-            not torch.cuda.is_current_stream_capturing()):
-        key = ("loop", X.data_ptr(), X.stride(0), F, int(K), out.data_ptr(), out.stride(0),
-               threshold, hub_threshold, bool(use_plan), G_rule, stream.value, PAD_X0)
+    if (not native_loop and hop_hook is None and prepare and X.data_ptr() != out.data_ptr()
+            and not torch.cuda.is_current_stream_capturing()):
+        key = ("list", X.stride(0), F, int(K), out.stride(0), X.data_ptr() % 128 == 0,
+               threshold, hub_threshold, bool(use_plan), G_rule, stream, PAD_X0)
         prep = csr._plans.get(key)
         if prep is not None:
-            with torch.cuda.device(X.device):
-                for fn, args in prep[1]:
-                    rc = fn(*args)
-                    if rc:
-                        _lib.check(rc, "propagate (prepared)")
+            rc = lib.sgc_launch_list_run(prep[1].handle, X.data_ptr(), out.data_ptr(), stream)
+            if rc:
+                _lib.check(rc, "propagate (launch list)")
             return out
     G = len(csr.groups_or_self(G_rule))
     if G > 1:
@@ -696,13 +698,16 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
         prepared = key is not None and n_bufs * n * ldw * 4 <= PREPARED_LOOP_MAX_BYTES
         bufs = [torch.empty((n, ldw), dtype=torch.float32, device=X.device)
                 for _ in range(n_bufs)]
-        launches = []  # (fn, args) of the loop, in order
+        ops = []  # the launches as recorded: (kind, args without the stream, src slot, dst slot)
+
+        def slot(t):
+            return SLOT_X0 if t is X else SLOT_OUT if t is out else SLOT_FIXED
         src, nxt = X, 0
         if pad:
-            launches.append((lib.sgc_pad_rows_f32, (_lib.ptr(X), X.stride(0), _lib.ptr(bufs[0]),
-                                                    ldw, n, F, stream)))
+            args = (_lib.ptr(X), X.stride(0), _lib.ptr(bufs[0]), ldw, n, F)
+            ops.append(("pad", args, SLOT_X0, SLOT_FIXED))
             src, nxt = bufs[0][:, :F], 1 % len(bufs)
-            _lib.check(launches[-1][0](*launches[-1][1]), "pad_rows_f32")
+            _lib.check(lib.sgc_pad_rows_f32(*args, stream), "pad_rows_f32")
         for h in range(K):
             dst = out if h == K - 1 else bufs[nxt][:, :F]
             # the engine's own buffers may be read / written in their pad columns
@@ -713,19 +718,46 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
             for c, cp, gflags in parts:  # column groups: 0 plain, 1.. accumulate
                 args = (_lib.ptr(c.row_ptr), _lib.ptr(c.col_idx), _lib.ptr(c.val), 0, n,
                         _lib.ptr(src), src.stride(0), _lib.ptr(dst), dst.stride(0), F,
-                        _lib.ptr(cp.rows), cp.n_heavy, cp.n_hub, cp.threshold, flags | gflags,
-                        stream)
-                launches.append((lib.sgc_spmm_csr_f32_ex, args))
-                _lib.check(lib.sgc_spmm_csr_f32_ex(*args), "spmm_csr_f32")
+                        _lib.ptr(cp.rows), cp.n_heavy, cp.n_hub, cp.threshold, flags | gflags)
+                ops.append(("spmm", args, slot(src), slot(dst)))
+                _lib.check(lib.sgc_spmm_csr_f32_ex(*args, stream), "spmm_csr_f32")
             if hop_hook:
                 hop_hook("end", h)
             src, nxt = dst, nxt ^ 1
         if prepared:
-            old = [k for k in csr._plans if isinstance(k, tuple) and k[:1] == ("loop",)]
+            old = [k for k in csr._plans if isinstance(k, tuple) and k[:1] == ("list",)]
             for k in old[:max(0, len(old) - PREPARED_LOOPS_KEPT + 1)]:
                 del csr._plans[k]  # oldest first (dicts keep insertion order)
-            csr._plans[key] = (bufs, launches, parts)  # parts: keep the pointers alive
+            csr._plans[key] = (bufs, LaunchList(ops), parts)  # parts: keep the pointers alive
     return out
+
+
+class LaunchList:
+    """A native launch list (sgc_launch_list_*) holding one propagate() loop:
+    the ops as recorded, X_0 / X_K by slot; destroyed with this object."""
+
+    __slots__ = ("handle", "_lib")
+
+    def __init__(self, ops):
+        import ctypes
+        lib = _lib.load()
+        h = ctypes.c_int64(0)
+        _lib.check(lib.sgc_launch_list_create(ctypes.byref(h)), "launch_list_create")
+        self.handle, self._lib = h.value, lib
+        for kind, args, s_src, s_dst in ops:
+            if kind == "pad":
+                rc = lib.sgc_launch_list_add_pad_rows(self.handle, *args, s_src, s_dst)
+            else:
+                rc = lib.sgc_launch_list_add_spmm(self.handle, *args, s_src, s_dst)
+            _lib.check(rc, "launch_list_add")
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self._lib.sgc_launch_list_destroy(self.handle)
+                self.handle = 0
+        except Exception:  # interpreter shutdown: the library may be gone
+            pass
 
 
 # propagate()'s prepared loops: at most this many bytes of intermediates each,

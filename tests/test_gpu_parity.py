@@ -815,26 +815,48 @@ def test_graphed_propagation_bit_exact(tiny_cases, name, K, hub):
 
 @pytest.mark.parametrize("name,K", [("norm_n48_F602", 3), ("hub1000_F130", 2), ("norm_n48_F65", 1)])
 def test_prepared_loop_replay_bit_exact(tiny_cases, name, K):
-    """propagate()'s prepared loop (second call with the same X / out / K):
-    the reference's bits, new contents of X picked up, a hop_hook call (the
-    unprepared loop) agreeing, and drop_groups() dropping the prepared loops."""
+    """propagate()'s recorded launch list (sgc_launch_list_*, second call with
+    the same shapes / K): the reference's bits, new contents of X picked up,
+    OTHER X_0 / X_K tensors of the same layout replayed through the same list
+    (X_0 and X_K enter by slot), an X_0 view at another 128-B alignment
+    recording its own list, a hop_hook call (the unrecorded loop) agreeing,
+    and drop_groups() dropping the lists."""
     from sgc_amd.propagate import DeviceCSR, propagate
     c = tiny_cases[name]
     csr = DeviceCSR.from_torch(coo_cuda(c))
     X = torch.from_numpy(c["X"]).to(DEV)
     out = torch.full_like(X, float("nan"))
+    lists = lambda: [k for k in csr._plans if isinstance(k, tuple) and k[0] == "list"]  # noqa: E731
     for _ in range(2):
         propagate(csr, X, K, out=out)
         torch.cuda.synchronize()
         assert bits_equal(out.cpu().numpy(), c[f"Y{K}"])
-    assert any(isinstance(k, tuple) and k[0] == "loop" for k in csr._plans)
+    assert len(lists()) == 1
     X.copy_(torch.flip(X, dims=[0]))
     want = propagate(csr, X, K, hop_hook=lambda *a: None).cpu().numpy()
     propagate(csr, X, K, out=out)
     torch.cuda.synchronize()
     assert bits_equal(out.cpu().numpy(), want)
+    # another X_0 and X_K of the same layout: the same list, their own pointers
+    X2 = torch.flip(X, dims=[0]).contiguous()
+    out2 = torch.full_like(X, float("nan"))
+    propagate(csr, X2, K, out=out2)
+    torch.cuda.synchronize()
+    assert len(lists()) == 1
+    assert bits_equal(out2.cpu().numpy(), c[f"Y{K}"])
+    assert bits_equal(out.cpu().numpy(), want)  # the first X_K untouched
+    # X_0 one row into a larger buffer: another 128-B alignment class
+    n, F = X.shape
+    big = torch.zeros((n + 1) * F + 1, device=DEV)
+    Xs = big[1:1 + n * F].view(n, F)
+    Xs.copy_(torch.from_numpy(c["X"]).to(DEV))
+    got = propagate(csr, Xs, K)
+    got = propagate(csr, Xs, K)  # replayed
+    torch.cuda.synchronize()
+    assert bits_equal(got.cpu().numpy(), c[f"Y{K}"])
+    assert len(lists()) == 2
     csr.drop_groups()
-    assert not any(isinstance(k, tuple) and k[0] == "loop" for k in csr._plans)
+    assert not lists()
 
 
 @pytest.mark.parametrize("r0,r1,th", [(0, 4000, 7), (123, 3001, 0), (0, 4000, 2**31 - 1), (50, 50, 5)])
