@@ -1163,9 +1163,11 @@ def _chunk_order(csr, chunks):
 #                     gather (the link's first work) is not slowed by the
 #                     chunk beside it;
 #  HUB_EARLY          the hub rows of the chunk holding the longest row run
-#                     first, on a stream of their own, the rest of that chunk
-#                     in its turn -- its serial chain no longer starts only
-#                     when the chunks before it are done; off: the hub launch
+#                     early, on a stream of their own (with FIRST_CHUNK_ALONE:
+#                     from the first chunk's end on, beside the chunks after
+#                     it; else from the start), the rest of that chunk in its
+#                     turn -- its serial chain no longer starts only when the
+#                     chunks before it are done.  Launched at the start it
 #                     delayed the first chunk by ~0.25 ms and every P=8
 #                     projection dropped (profiles/r05/rehearsal_sched.log).
 FIRST_CHUNK_ALONE = True
@@ -1199,13 +1201,20 @@ def _replicated_last_hop(prop, n, P, p, ld, X0, hop_into, gather, unpack):
     chunks = replicated_chunks(n, REPLICATED_CHUNKS if prop.chunks == 4 else (1,) * prop.chunks)
     order = _chunk_order(getattr(prop, "csr", None), chunks)
     hub_split = gpu and HUB_EARLY and len(order) > 1
-    if hub_split:  # the hub chunk's hub rows first, beside everything else
+
+    def hub_rows_first(after):
+        # the hub chunk's hub rows, on a stream of their own from `after` on
         sh = prop._chunk_streams[2]
-        sh.wait_stream(cur)
+        if isinstance(after, torch.cuda.Event):
+            sh.wait_event(after)
+        else:
+            sh.wait_stream(after)
         r0, r1 = chunks[order[-1]]
         full = prop._buf(("full", order[-1]), (P * (r1 - r0), ld), X0)
         with torch.cuda.stream(sh):
             hop_into(r0, r1, _gather_slot(full, p, r1 - r0), SPMM_HUB_ONLY)
+    if hub_split and not FIRST_CHUNK_ALONE:
+        hub_rows_first(cur)
     first_done = None
     for i, ci in enumerate(order):
         r0, r1 = chunks[ci]
@@ -1223,6 +1232,8 @@ def _replicated_last_hop(prop, n, P, p, ld, X0, hop_into, gather, unpack):
                 if i == 0 and FIRST_CHUNK_ALONE:
                     first_done = torch.cuda.Event()
                     first_done.record(st)
+                    if hub_split:  # beside the chunks after the first
+                        hub_rows_first(first_done)
                 if split:
                     st.wait_stream(prop._chunk_streams[2])
                 work = gather(full, loc)
