@@ -708,7 +708,13 @@ hipError_t launch_stream(const float *X, int64_t ldx, const float *W, const floa
     return hipGetLastError();
 }
 
-constexpr int kSplitWaves = 8;
+#ifndef SGC_SPLIT_WAVES
+#define SGC_SPLIT_WAVES 8
+#endif
+// waves of the one workgroup per CU: 8 (12 or 16 measured 0.145 / 0.138 vs
+// 0.089 ms: the register budget at 3-4 waves per SIMD spills the ring,
+// profiles/r05/linear_ab_waves.log)
+constexpr int kSplitWaves = SGC_SPLIT_WAVES;
 
 // Split-bf16 kernel: W's operand image (split_chunk_bytes per 32-k chunk) +
 // the tile counter.
