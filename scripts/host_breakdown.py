@@ -99,6 +99,13 @@ def main():
     rec["bare_enqueue_us"] = med(bare, min(a.reps, 200))
     torch.cuda.synchronize()
     rec["bare_devsync_us"] = med(lambda: (bare(), torch.cuda.synchronize()), a.reps)
+    def spin():
+        ev = torch.cuda.Event()
+        ev.record()
+        while not ev.query():
+            pass
+    rec["bare_eventspin_us"] = med(lambda: (bare(), spin()), a.reps)
+    rec["propagate_eventspin_us"] = med(lambda: (propagate(csr, X, K, out=out), spin()), a.reps)
     rec["trivial_ctypes_call_us"] = med(lambda: lib.sgc_get_tuning(b"slice_floats"), a.reps)
     print(json.dumps(rec), flush=True)
 
