@@ -246,7 +246,7 @@ class DeviceCSR:
         """Free the cached column-group copies of S (and their plans): one
         more col/val copy per G (188 MB at Reddit shape).  They are rebuilt
         on the next launch that uses them."""
-        self.release_prepared()  # prepared loops hold the groups' pointers
+        self.release_prepared()  # recorded launch lists hold the groups' pointers
         for key in [k for k in self._plans if isinstance(k, tuple) and k[:1] == ("groups",)]:
             for part in self._plans.pop(key):
                 part._plans.clear()
@@ -621,7 +621,7 @@ def propagate(csr: DeviceCSR, X: torch.Tensor, K: int, out=None, use_plan=True, 
     last hop writes the contiguous [N, F] result.  hop_hook(phase, h) is called
     around each hop's launch ("start"/"end", for event timing).
     native_loop=True runs the same loop inside the C ABI call instead.
-    prepare=False neither replays nor keeps a prepared loop (GraphedPropagation's
+    prepare=False neither replays nor records a launch list (GraphedPropagation's
     warm-up and capture; nothing is kept under a stream capture either)."""
     X = check_propagation_inputs(csr, X)
     n, F = X.shape
@@ -760,7 +760,7 @@ class LaunchList:
             pass
 
 
-# propagate()'s prepared loops: at most this many bytes of intermediates each,
+# propagate()'s recorded launch lists: at most this many bytes of intermediates each,
 # and this many (X, out, K, stream) combinations per adjacency
 PREPARED_LOOP_MAX_BYTES = 1 << 26
 PREPARED_LOOPS_KEPT = 4
@@ -794,7 +794,7 @@ class GraphedPropagation:
         csr.plan(0, n, threshold, hub_threshold, F)  # synchronous: never inside the capture
         side = torch.cuda.Stream(device=csr.device)
         side.wait_stream(torch.cuda.current_stream(csr.device))
-        with torch.cuda.stream(side):  # (no prepared loop kept for the side stream)
+        with torch.cuda.stream(side):  # (no launch list kept for the side stream)
             propagate(csr, self.x_in, self.K, out=self.out, prepare=False, **kw)
         torch.cuda.current_stream(csr.device).wait_stream(side)
         torch.cuda.synchronize(csr.device)
