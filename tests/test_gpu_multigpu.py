@@ -162,6 +162,69 @@ def test_mgpu_handles_survive_reinit(tiny_cases, oracle):
 
 
 # ---------------------------------------------------------------------------
+# the exchanges' block copy (sgc_copy_blocks_f32, csrc/exchange.hip)
+
+@pytest.mark.parametrize("lds,ldd,align", [(64, 602, 4), (76, 602, 2), (96, 608, 4),
+                                           (33, 101, 1), (512, 512, 4)])
+def test_copy_blocks_matches_slicing(lds, ldd, align):
+    """One launch lands up to 64 (src_row, src_col, dst_row, dst_col, rows,
+    cols) blocks -- the replicated output's unpack: P column blocks of a
+    gathered [P*rows, ld] chunk into X_K's columns, ragged last block, empty
+    segments -- exactly as the torch slice copies; 16-B / 8-B / 4-B vectors
+    by the strides and offsets, segments longer than the grid (grid-stride
+    loop); untouched elements stay."""
+    from sgc_amd.distributed import _copy_blocks
+    rng = np.random.default_rng(lds * 1000 + ldd)
+    rows_src, rows_dst = 9000, 5000
+    src = torch.from_numpy(rng.standard_normal((rows_src, lds), dtype=np.float32)).to("cuda")
+    dst = torch.full((rows_dst, ldd), float("nan"), device="cuda")
+    segs, q, c = [], 0, 0
+    while c < ldd and q < 60:
+        w = int(min(ldd - c, rng.integers(1, lds + 1) // align * align or align))
+        w = min(w, lds)
+        r = int(rng.integers(0, 1400))
+        sr = int(rng.integers(0, rows_src - r + 1))
+        dr = int(rng.integers(0, rows_dst - r + 1))
+        sc = int(rng.integers(0, (lds - w) // align + 1)) * align
+        segs.append((sr, sc, dr, c, r, w))
+        c += w
+        q += 1
+    segs.append((0, 0, 0, 0, 0, 5))  # empty
+    want = dst.clone()
+    for sr, sc, dr, dc, r, w in segs:
+        want[dr:dr + r, dc:dc + w] = src[sr:sr + r, sc:sc + w]
+    _copy_blocks(src, dst, segs)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.nan_to_num(dst, nan=7.0), torch.nan_to_num(want, nan=7.0))
+    # whole 64-block chunk in one launch: the P = 64 limit
+    full = torch.from_numpy(rng.standard_normal((64 * 300, 8), dtype=np.float32)).to("cuda")
+    out = torch.zeros((300, 64 * 8), device="cuda")
+    _copy_blocks(full, out, [(qq * 300, 0, 0, qq * 8, 300, 8) for qq in range(64)])
+    torch.cuda.synchronize()
+    assert torch.equal(out, full.view(64, 300, 8).permute(1, 0, 2).reshape(300, 512))
+
+
+def test_copy_blocks_rejects_bad_segments():
+    """More than 64 segments, a block past the row stride, negative sizes:
+    SGCError, nothing launched."""
+    import ctypes
+    from sgc_amd import _lib
+    lib = _lib.load()
+    src = torch.zeros((10, 8), device="cuda")
+    dst = torch.zeros((10, 8), device="cuda")
+
+    def call(segs):
+        arr = (ctypes.c_int64 * (6 * len(segs)))(*[v for sg in segs for v in sg])
+        return lib.sgc_copy_blocks_f32(_lib.ptr(src), 8, _lib.ptr(dst), 8, len(segs), arr,
+                                       _lib.stream_handle())
+    assert call([(0, 0, 0, 0, 1, 1)] * 65) != 0
+    assert call([(0, 4, 0, 0, 1, 8)]) != 0
+    assert call([(0, 0, 0, 0, -1, 1)]) != 0
+    assert call([(0, 0, 0, 0, 10, 8)]) == 0
+    torch.cuda.synchronize()
+
+
+# ---------------------------------------------------------------------------
 # sgc_precompute under torchrun, the reddit driver, bench.py self-launch
 
 @pytest.mark.parametrize("partition", ["features", "lines", "rows", "cyclic", "replicate", "auto"])
