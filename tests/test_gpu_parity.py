@@ -859,6 +859,37 @@ def test_prepared_loop_replay_bit_exact(tiny_cases, name, K):
     assert not lists()
 
 
+def test_launch_list_abi_errors(tiny_cases):
+    """sgc_launch_list_*: unknown handles, bad slots and a slot run without its
+    pointer are errors (no launch); destroy frees the handle once; a list of
+    one hop with both slots replays bit-exactly."""
+    import ctypes
+    from sgc_amd import _lib
+    from sgc_amd.propagate import DeviceCSR, propagate
+    lib = _lib.load()
+    c = tiny_cases["norm_n48_F602"]
+    csr = DeviceCSR.from_torch(coo_cuda(c))
+    X = torch.from_numpy(c["X"]).to(DEV)
+    n, F = X.shape
+    out = torch.full_like(X, float("nan"))
+    s = _lib.stream_handle()
+    assert lib.sgc_launch_list_run(987654321, _lib.ptr(X), _lib.ptr(out), s) != 0
+    assert lib.sgc_launch_list_destroy(987654321) != 0
+    h = ctypes.c_int64(0)
+    _lib.check(lib.sgc_launch_list_create(ctypes.byref(h)), "create")
+    args = (_lib.ptr(csr.row_ptr), _lib.ptr(csr.col_idx), _lib.ptr(csr.val), 0, n, None, F, None,
+            F, F, None, 0, 0, 0, 0)
+    assert lib.sgc_launch_list_add_spmm(h.value, *args, 3, 2) != 0      # bad slot
+    assert lib.sgc_launch_list_add_spmm(h.value, *args[:-1], 1 << 20, 1, 2) != 0  # unknown flag
+    _lib.check(lib.sgc_launch_list_add_spmm(h.value, *args, 1, 2), "add")
+    assert lib.sgc_launch_list_run(h.value, None, _lib.ptr(out), s) != 0  # X_0 slot, no X_0
+    _lib.check(lib.sgc_launch_list_run(h.value, _lib.ptr(X), _lib.ptr(out), s), "run")
+    torch.cuda.synchronize()
+    assert bits_equal(out.cpu().numpy(), propagate(csr, X, 1, prepare=False).cpu().numpy())
+    _lib.check(lib.sgc_launch_list_destroy(h.value), "destroy")
+    assert lib.sgc_launch_list_destroy(h.value) != 0
+
+
 @pytest.mark.parametrize("r0,r1,th", [(0, 4000, 7), (123, 3001, 0), (0, 4000, 2**31 - 1), (50, 50, 5)])
 def test_plan_light_order(r0, r1, th):
     """sgc_plan_light_order: the light rows (degree <= threshold) of the range,
