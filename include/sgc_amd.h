@@ -387,6 +387,28 @@ int sgc_linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_
                             int64_t M, int64_t K, int64_t C, float *dW, float *db,
                             void *workspace, int64_t workspace_bytes, void *stream);
 
+/* Softmax cross-entropy over a logits matrix: the loss the reference's
+ * closures take of the classifier's output, F.cross_entropy(model(x), y)
+ * with mean reduction (citation.py:46-49, reddit.py:55-58), and its
+ * gradient.  logits [M, C] (row stride ldl, C <= 64), labels int64 [M]; rows
+ * whose label equals ignore_index are left out of the mean (torch's
+ * default is -100).  Forward: *loss = mean over the counted rows of
+ * lse_m - logits[m, y_m], lse[m] = log sum_c exp(logits[m, c]) (kept for the
+ * backward), *inv_count = 1 / (counted rows); NaN loss for a label outside
+ * [0, C).  Backward: dlogits = (softmax - onehot) * (*grad_loss) *
+ * (*inv_count) (grad_loss may be NULL: 1), zero rows for ignored labels.
+ * Device scalars throughout (no host synchronisation).  Deterministic;
+ * tolerance-equal to torch (rtol 1e-5).  workspace:
+ * sgc_cross_entropy_workspace(M, C) bytes. */
+int64_t sgc_cross_entropy_workspace(int64_t M, int64_t C);
+int sgc_cross_entropy_f32(const float *logits, int64_t ldl, const int64_t *labels, int64_t M,
+                          int64_t C, int64_t ignore_index, float *loss, float *inv_count,
+                          float *lse, void *workspace, int64_t workspace_bytes, void *stream);
+int sgc_cross_entropy_backward_f32(const float *logits, int64_t ldl, const int64_t *labels,
+                                   const float *lse, const float *inv_count,
+                                   const float *grad_loss, int64_t M, int64_t C,
+                                   int64_t ignore_index, float *dlogits, int64_t ldd, void *stream);
+
 /* ---------------------------------------------------------------------------
  * Fused classifier training step: for the SGC closure
  * (citation.py:46-49, reddit.py:55-58: F.cross_entropy(model(x), y) then
@@ -513,7 +535,7 @@ int sgc_mgpu_finalize(void);
  * `stream` (the current device) and waits for them, so those loads happen
  * here rather than inside the first sgc_precompute the caller times
  * (reddit.py:43,72-74).  Units: SGC_WARM_PROPAGATE = SpMM, ingest, plan,
- * sort, column groups, the exchanges' block copy; SGC_WARM_CLASSIFIER = linear, fused loss;
+ * sort, column groups, the exchanges' block copy; SGC_WARM_CLASSIFIER = linear, fused loss, cross-entropy;
  * SGC_WARM_LOADERS = normalisation, sub-graph.  Synchronous. */
 enum { SGC_WARM_PROPAGATE = 1, SGC_WARM_CLASSIFIER = 2, SGC_WARM_LOADERS = 4 };
 int sgc_warmup(uint32_t units, void *stream);

@@ -14,7 +14,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libsgc_amd.so")
 SOURCES = ["capi.hip", "spmm.hip", "ingest.hip", "linear.hip", "normalize.hip", "xent.hip",
            "subgraph.hip", "cpu.hip", "mgpu.hip", "plan.hip", "groups.hip", "sort.hip",
-           "exchange.hip"]
+           "exchange.hip", "loss.hip"]
 
 
 def _headers():

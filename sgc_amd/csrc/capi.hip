@@ -53,6 +53,13 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
                     const int64_t *labels, int64_t M, int64_t K, int64_t C, float *loss,
                     float *dW, float *db, float *logits, int64_t ldl, void *ws, int64_t ws_bytes,
                     hipStream_t s);
+int64_t cross_entropy_workspace(int64_t M, int64_t C);
+int cross_entropy_fwd_f32(const float *Y, int64_t ldy, const int64_t *labels, int64_t M, int64_t C,
+                          int64_t ignore_index, float *loss, float *inv_count, float *lse, void *ws,
+                          int64_t ws_bytes, hipStream_t s);
+int cross_entropy_bwd_f32(const float *Y, int64_t ldy, const int64_t *labels, const float *lse,
+                          const float *inv_count, const float *grad, int64_t M, int64_t C,
+                          int64_t ignore_index, float *dY, int64_t lddy, hipStream_t s);
 int64_t linear_backward_workspace_bytes(int64_t M, int64_t K, int64_t C);
 int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ldd, int64_t M,
                         int64_t K, int64_t C, float *dW, float *db, void *ws, int64_t ws_bytes,
@@ -481,6 +488,23 @@ int sgc_linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_
                                as_stream(stream));
 }
 
+int64_t sgc_cross_entropy_workspace(int64_t M, int64_t C) { return cross_entropy_workspace(M, C); }
+
+int sgc_cross_entropy_f32(const float *logits, int64_t ldl, const int64_t *labels, int64_t M,
+                          int64_t C, int64_t ignore_index, float *loss, float *inv_count,
+                          float *lse, void *workspace, int64_t workspace_bytes, void *stream) {
+    return cross_entropy_fwd_f32(logits, ldl, labels, M, C, ignore_index, loss, inv_count, lse,
+                                 workspace, workspace_bytes, as_stream(stream));
+}
+
+int sgc_cross_entropy_backward_f32(const float *logits, int64_t ldl, const int64_t *labels,
+                                   const float *lse, const float *inv_count,
+                                   const float *grad_loss, int64_t M, int64_t C,
+                                   int64_t ignore_index, float *dlogits, int64_t ldd, void *stream) {
+    return cross_entropy_bwd_f32(logits, ldl, labels, lse, inv_count, grad_loss, M, C,
+                                 ignore_index, dlogits, ldd, as_stream(stream));
+}
+
 int64_t sgc_linear_xent_workspace(int64_t M, int64_t K, int64_t C) {
     return xent_workspace_bytes(M, K, C);
 }
@@ -507,6 +531,7 @@ int sgc_warmup(uint32_t units, void *stream) {
     if (units & SGC_WARM_CLASSIFIER) {
         SGC_HIP_CHECK(warm_linear(s));
         SGC_HIP_CHECK(warm_xent(s));
+        SGC_HIP_CHECK(warm_loss(s));
     }
     if (units & SGC_WARM_LOADERS) {
         SGC_HIP_CHECK(warm_normalize(s));

@@ -51,6 +51,7 @@ hipError_t warm_groups(hipStream_t);
 hipError_t warm_exchange(hipStream_t);
 hipError_t warm_linear(hipStream_t);
 hipError_t warm_xent(hipStream_t);
+hipError_t warm_loss(hipStream_t);
 hipError_t warm_normalize(hipStream_t);
 hipError_t warm_subgraph(hipStream_t);
 

@@ -8,7 +8,11 @@ On ROCm tensors the forward GEMM runs on the fp32 MFMA kernel
 one read of X: sgc_linear_backward_f32) on the same MFMA tile -- what the
 reference closures' .backward() needs (citation.py:47-49, reddit.py:55-58);
 dX = dY W (only if the features require a gradient) is a torch op.  Adam
-(citation.py:41) and LBFGS (reddit.py:52) work unchanged.  On CPU tensors (the reference's --no-cuda mode) the forward is the
+(citation.py:41) and LBFGS (reddit.py:52) work unchanged.  The ROCm output is
+an SGCLogits tensor: the closures' unchanged F.cross_entropy(output, labels)
+runs on the HIP cross-entropy kernels (sgc_cross_entropy_f32, one pass for
+the loss, one for the gradient) rather than torch's nll reduction.  On CPU
+tensors (the reference's --no-cuda mode) the forward is the
 reference's own nn.Linear arithmetic, so CPU runs reproduce its results bit
 for bit.
 """
@@ -65,6 +69,93 @@ class _LinearCrossEntropy(torch.autograd.Function):
         return None, grad_loss * dW, (grad_loss * db if ctx.has_bias else None), None
 
 
+class _LogitsCrossEntropy(torch.autograd.Function):
+    """F.cross_entropy(logits, labels) (mean, ignore_index) on the HIP kernels
+    (sgc_cross_entropy_f32 / _backward_f32): the loss and the per-row
+    log-sum-exp in one pass, the logits' gradient in one more -- scaled by
+    the incoming gradient on the device, no host synchronisation."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        from . import _lib
+        lib = _lib.load()
+        M, C = logits.shape
+        dev = logits.device
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        inv = torch.empty(1, dtype=torch.float32, device=dev)
+        lse = torch.empty(M, dtype=torch.float32, device=dev)
+        ws_bytes = lib.sgc_cross_entropy_workspace(M, C)
+        ws = torch.empty(max(1, ws_bytes), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            _lib.check(lib.sgc_cross_entropy_f32(_lib.ptr(logits), logits.stride(0), _lib.ptr(labels),
+                                                 M, C, int(ignore_index), _lib.ptr(loss), _lib.ptr(inv),
+                                                 _lib.ptr(lse), _lib.ptr(ws), ws_bytes,
+                                                 _lib.stream_handle(dev)), "cross_entropy_f32")
+        ctx.save_for_backward(logits, labels, lse, inv)
+        ctx.ignore_index = int(ignore_index)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        from . import _lib
+        logits, labels, lse, inv = ctx.saved_tensors
+        M, C = logits.shape
+        dY = torch.empty((M, C), dtype=torch.float32, device=logits.device)
+        g = grad_loss.detach().to(torch.float32).contiguous()
+        with torch.cuda.device(logits.device):
+            _lib.check(_lib.load().sgc_cross_entropy_backward_f32(
+                _lib.ptr(logits), logits.stride(0), _lib.ptr(labels), _lib.ptr(lse), _lib.ptr(inv),
+                _lib.ptr(g), M, C, ctx.ignore_index, _lib.ptr(dY), dY.stride(0),
+                _lib.stream_handle(logits.device)), "cross_entropy_backward_f32")
+        return dY, None, None
+
+
+def _cross_entropy_args(args, kwargs):
+    """(logits, labels, ignore_index) when F.cross_entropy(*args, **kwargs) is
+    the plain form the HIP kernels compute (mean reduction, no class weights,
+    no label smoothing, int64 class-index labels, C <= 64), else None."""
+    names = ("input", "target", "weight", "size_average", "ignore_index", "reduce", "reduction",
+             "label_smoothing")
+    bound = dict(zip(names, args))
+    for k, v in kwargs.items():
+        if k in bound or k not in names:
+            return None
+        bound[k] = v
+    x, y = bound.get("input"), bound.get("target")
+    if (bound.get("weight") is not None or bound.get("size_average") is not None or
+            bound.get("reduce") is not None or bound.get("reduction", "mean") != "mean" or
+            bound.get("label_smoothing", 0.0) != 0.0):
+        return None
+    if not (isinstance(x, torch.Tensor) and isinstance(y, torch.Tensor)):
+        return None
+    if (x.dim() != 2 or x.dtype != torch.float32 or x.device.type != "cuda" or
+            not 0 < x.shape[1] <= 64 or x.shape[0] == 0 or x.stride(1) != 1 or
+            y.dim() != 1 or y.dtype != torch.int64 or y.device != x.device or
+            y.shape[0] != x.shape[0]):
+        return None
+    return x, y.contiguous(), int(bound.get("ignore_index", -100))
+
+
+class SGCLogits(torch.Tensor):
+    """The ROCm classifier's output (SGC.forward): an ordinary logits tensor
+    that routes ``F.cross_entropy(logits, labels)`` -- the reference closures'
+    loss (citation.py:46-49, reddit.py:55-58), called unchanged -- to the HIP
+    cross-entropy kernels (_LogitsCrossEntropy) instead of torch's one-
+    workgroup nll reduction; any other form of the call and every other
+    operation is torch's own and returns plain tensors."""
+
+    @classmethod
+    def __torch_function__(cls, func, types, args=(), kwargs=None):
+        kwargs = kwargs or {}
+        if func is F.cross_entropy:
+            plain = _cross_entropy_args(args, kwargs)
+            if plain is not None:
+                x, y, ignore_index = plain
+                return _LogitsCrossEntropy.apply(x.as_subclass(torch.Tensor), y, ignore_index)
+        with torch._C.DisableTorchFunctionSubclass():
+            return func(*args, **kwargs)
+
+
 def sgc_cross_entropy(model, features, labels):
     """F.cross_entropy(model(features), labels) for an SGC model, fused on the
     GPU: one launch chain computes the loss and the W/b gradients (the
@@ -86,7 +177,8 @@ class SGC(nn.Module):
     def forward(self, x):
         if x.device.type == "cpu":  # reference arithmetic (models.py:18)
             return self.W(x)
-        return _LinearMFMA.apply(x, self.W.weight, self.W.bias)
+        # (a logits tensor whose F.cross_entropy runs on the HIP kernels)
+        return _LinearMFMA.apply(x, self.W.weight, self.W.bias).as_subclass(SGCLogits)
 
 
 def get_model(model_opt, nfeat, nclass, nhid=0, dropout=0, cuda=True):

@@ -764,6 +764,88 @@ def test_fused_xent_matches_torch(M, K, C):
     assert torch.equal(loss, loss2) and torch.equal(dW, dW2) and torch.equal(db, db2)
 
 
+@pytest.mark.parametrize("M,C,ldl", [(1, 1, 1), (7, 2, 5), (1000, 41, 41), (4099, 64, 64),
+                                     (152410, 41, 41), (333, 17, 20), (5000, 3, 3)])
+def test_logits_cross_entropy_matches_torch(M, C, ldl):
+    """F.cross_entropy on SGCLogits (the reference closures' call, unchanged)
+    runs sgc_cross_entropy_f32 / _backward_f32: loss and dlogits vs fp64
+    torch (fp32 tolerance), ignore_index rows (-100 and a custom one) left
+    out of the mean, strided logits, the incoming gradient scaled on the
+    device, bitwise reproducible; a non-plain call (reduction="sum", label
+    smoothing) is torch's own."""
+    from sgc_amd.models import SGCLogits
+    F_ = torch.nn.functional
+    g = torch.Generator().manual_seed(M + C)
+    base = torch.randn((M, ldl), generator=g) * 3
+    y0 = torch.randint(0, C, (M,), generator=g)
+    for ign in (-100, 1 % C):
+        y = y0.clone()
+        if M > 3:
+            y[::7] = ign
+        ref_x = base[:, :C].double().requires_grad_()
+        ref = F_.cross_entropy(ref_x, y, ignore_index=ign)
+        (ref * 3).backward()
+        full = base.to(DEV).requires_grad_()
+        xg = full[:, :C]  # row stride ldl
+        logits = xg.as_subclass(SGCLogits)
+        loss = F_.cross_entropy(logits, y.to(DEV), ignore_index=ign)
+        assert type(loss) is torch.Tensor and loss.grad_fn is not None
+        assert "LogitsCrossEntropy" in type(loss.grad_fn).__name__
+        (loss * 3).backward()
+        # (every row ignored, M = 1: NaN on both sides, as a mean over no rows)
+        torch.testing.assert_close(loss.detach().cpu().double(), ref.detach(), rtol=1e-5, atol=1e-6,
+                                   equal_nan=True)
+        torch.testing.assert_close(full.grad[:, :C].cpu().double(), ref_x.grad, rtol=1e-4,
+                                   atol=1e-7, equal_nan=True)
+        loss2 = F_.cross_entropy(logits, y.to(DEV), ignore_index=ign)
+        assert torch.equal(loss.detach(), loss2.detach()) or torch.isnan(loss2).item()
+    s = F_.cross_entropy(base.to(DEV)[:, :C].as_subclass(SGCLogits), y0.to(DEV), reduction="sum")
+    assert type(s) is torch.Tensor
+    torch.testing.assert_close(s.cpu().double(), F_.cross_entropy(base[:, :C].double(), y0,
+                                                                  reduction="sum"),
+                               rtol=1e-5, atol=1e-4)
+
+
+def test_logits_cross_entropy_bad_label_gives_nan():
+    """A label outside [0, C) (not ignore_index): the loss is NaN (torch
+    stops with a device assert), no fault."""
+    from sgc_amd.models import SGCLogits
+    x = torch.randn(50, 5, device=DEV).as_subclass(SGCLogits)
+    y = torch.randint(0, 5, (50,), device=DEV)
+    y[3] = 9
+    assert torch.isnan(torch.nn.functional.cross_entropy(x, y)).item()
+
+
+def test_unchanged_closure_uses_the_hip_loss():
+    """The reference closure as written (citation.py:46-49, reddit.py:55-58:
+    zero_grad; F.cross_entropy(model(x), y).backward()) on the drop-in SGC:
+    the loss is the HIP kernel's, W / b gradients match nn.Linear + torch's
+    loss (fp32 tolerance); eval ops on the logits return plain tensors."""
+    from sgc_amd.models import SGC, SGCLogits
+    torch.manual_seed(1)
+    m = SGC(602, 41).to(DEV)
+    ref = torch.nn.Linear(602, 41).to(DEV)
+    ref.load_state_dict(m.W.state_dict())
+    x = torch.randn(3000, 602, device=DEV)
+    y = torch.randint(0, 41, (3000,), device=DEV)
+    m.zero_grad()
+    out = m(x)
+    assert isinstance(out, SGCLogits)
+    loss = torch.nn.functional.cross_entropy(out, y)
+    assert "LogitsCrossEntropy" in type(loss.grad_fn).__name__
+    loss.backward()
+    lref = torch.nn.functional.cross_entropy(ref(x), y)
+    lref.backward()
+    torch.testing.assert_close(loss, lref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(m.W.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(m.W.bias.grad, ref.bias.grad, rtol=1e-4, atol=1e-6)
+    preds = out.max(1)[1]
+    assert type(preds) is torch.Tensor and type(out.detach().cpu()) is torch.Tensor
+    with torch.no_grad():
+        lv = torch.nn.functional.cross_entropy(m(x), y)
+    torch.testing.assert_close(lv, lref.detach(), rtol=1e-5, atol=1e-5)
+
+
 def test_fused_loss_trains_like_torch():
     """LBFGS (reddit.py's optimiser) with the fused loss tracks the unfused path."""
     from sgc_amd.models import SGC, sgc_cross_entropy
