@@ -114,6 +114,15 @@ __global__ __launch_bounds__(256) void xent_fwd_kernel(
     }
 }
 
+#ifndef SGC_DW_SLABS
+#define SGC_DW_SLABS 512
+#endif
+// dW partial slabs (workgroups of xent_dw_kernel) at most: each writes a
+// C16 x K partial that the reduction reads back.  512 measured best at the
+// Reddit-train shape: backward 0.142 ms vs 0.170 (256) and 0.191 (1024),
+// profiles/r05/bwd_slabs_ab.log.
+constexpr int64_t kDwSlabs = SGC_DW_SLABS;
+
 // ---- B: dW partial slabs -----------------------------------------------------
 constexpr int kDwDepth = 4;  // 4-row steps of G and X in flight per wave
 
@@ -348,7 +357,7 @@ int64_t xent_workspace_bytes(int64_t M, int64_t K, int64_t C) {
     if (M <= 0 || K <= 0 || C <= 0) return 0;
     const int64_t C16 = (C + 15) / 16 * 16;
     const int64_t waves = (M + kLdsBM - 1) / kLdsBM * 4;
-    const int64_t n_slabs = std::min<int64_t>(512, (M + 255) / 256);
+    const int64_t n_slabs = std::min<int64_t>(kDwSlabs, (M + 255) / 256);
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     return al(M * C16 * 4) + al(waves * 8) + al(waves * C16 * 4) + al(n_slabs * C16 * K * 4) + 512;
 }
@@ -372,7 +381,7 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
     const int NT = (int)((C + 15) / 16);
     const int C16 = NT * 16;
     const int waves = (int)((M + kLdsBM - 1) / kLdsBM * 4);
-    const int n_slabs = (int)std::min<int64_t>(512, (M + 255) / 256);
+    const int n_slabs = (int)std::min<int64_t>(kDwSlabs, (M + 255) / 256);
     const int rows_per = (int)(((M + n_slabs - 1) / n_slabs + 3) / 4 * 4);
     SGC_REQUIRE(dw_slab_fits(rows_per, ldx, NT * 16), SGC_ERANGE,
                 "classifier dW: %d rows x ldx %lld past the kernel's 31-bit offsets", rows_per,
@@ -445,7 +454,7 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
 int64_t linear_backward_workspace_bytes(int64_t M, int64_t K, int64_t C) {
     if (M <= 0 || K <= 0 || C <= 0) return 0;
     const int64_t C16 = (C + 15) / 16 * 16;
-    const int64_t n_slabs = std::min<int64_t>(512, (M + 255) / 256);
+    const int64_t n_slabs = std::min<int64_t>(kDwSlabs, (M + 255) / 256);
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     return al(n_slabs * C16 * K * 4) + al(n_slabs * C16 * 4) + 512;
 }
@@ -464,7 +473,7 @@ int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ld
                 (long long)ws_bytes, (long long)need);
     const int NT = (int)((C + 15) / 16);
     const int C16 = NT * 16;
-    const int n_slabs = (int)std::min<int64_t>(512, (M + 255) / 256);
+    const int n_slabs = (int)std::min<int64_t>(kDwSlabs, (M + 255) / 256);
     const int rows_per = (int)(((M + n_slabs - 1) / n_slabs + 3) / 4 * 4);
     SGC_REQUIRE(dw_slab_fits(rows_per, ldx, ldd), SGC_ERANGE,
                 "classifier dW: %d rows x ldx %lld past the kernel's 31-bit offsets", rows_per,
