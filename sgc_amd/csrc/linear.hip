@@ -16,6 +16,7 @@
 #include <utility>
 
 #include "gemm_tile.h"
+#include "split_bf16.h"
 
 namespace sgc {
 
@@ -317,25 +318,7 @@ constexpr int kSplitDepth = 4;  // chunks in flight per wave (the ring's slots)
 // counted waits drain the ring.  Held, a wave stores after its last load
 // (~4.7 tiles per wave at the Reddit-train shape; a seventh flushes the six).
 constexpr int kSplitHeld = SGC_SPLIT_HELD;
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
 template <int U> struct SlotC { static constexpr int value = U; };
-
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
-    const bf16x2_t v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32 (RNE)
-    return __builtin_bit_cast(uint32_t, v);
-}
-
-// (a, b) -> packed hi / mid / lo bf16 pairs with a == hi + mid + lo exactly
-// (finite a, b).
-__device__ __forceinline__ void split3(float a, float b, uint32_t &h, uint32_t &m, uint32_t &l) {
-    h = pk_bf16(a, b);
-    const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
-    m = pk_bf16(ra, rb);
-    l = pk_bf16(ra - __uint_as_float(m << 16), rb - __uint_as_float(m & 0xffff0000u));
-}
 
 __device__ __forceinline__ float ror8(float x) {  // lane j of each 16-lane row gets lane j ^ 8's x
     return __builtin_bit_cast(
