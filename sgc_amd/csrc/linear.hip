@@ -308,7 +308,13 @@ __global__ __launch_bounds__(64 * kStreamWaves) void linear_stream_kernel(
 // * The ring of D chunks per wave runs across tiles with compile-time slots
 //   (a rolled ring moved registers and selected slots at run time: ~100 extra
 //   VALU per chunk).
-constexpr int kSplitDepth = 4;  // chunks in flight per wave (the ring's slots)
+#ifndef SGC_SPLIT_DEPTH
+#define SGC_SPLIT_DEPTH 4
+#endif
+// chunks in flight per wave (the ring's slots): 4; 6 or 8 stream the loads
+// alone 1-2 % faster but the kernel no faster (0.092-0.093 vs 0.090-0.091 ms,
+// profiles/r05/linear_ab_depth.log)
+constexpr int kSplitDepth = SGC_SPLIT_DEPTH;
 #ifndef SGC_SPLIT_HELD
 #define SGC_SPLIT_HELD 6
 #endif
@@ -319,6 +325,25 @@ constexpr int kSplitDepth = 4;  // chunks in flight per wave (the ring's slots)
 // (~4.7 tiles per wave at the Reddit-train shape; a seventh flushes the six).
 constexpr int kSplitHeld = SGC_SPLIT_HELD;
 template <int U> struct SlotC { static constexpr int value = U; };
+
+// f(SlotC<U>{}) for U = U0 .. D-1 in order, compile-time slots (run_slots
+// stops at the first false and returns false).
+template <int U, int D, typename F>
+__device__ __forceinline__ void each_slot(F &&f) {
+    if constexpr (U < D) {
+        f(SlotC<U>{});
+        each_slot<U + 1, D>(f);
+    }
+}
+template <int U, int D, typename F>
+__device__ __forceinline__ bool run_slots(F &&f) {
+    if constexpr (U < D) {
+        if (!f(SlotC<U>{})) return false;
+        return run_slots<U + 1, D>(f);
+    } else {
+        return true;
+    }
+}
 
 __device__ __forceinline__ float ror8(float x) {  // lane j of each 16-lane row gets lane j ^ 8's x
     return __builtin_bit_cast(
@@ -371,7 +396,7 @@ __global__ __launch_bounds__(64 * NW) void linear_split_kernel(
     };
     rows_of(ltile);
     constexpr int D = kSplitDepth;
-    static_assert(D == 4, "the ring's slots are unrolled by hand below");
+    static_assert(D >= 2 && D <= 8, "ring depth");
     f4 xa[D], xb[D];
     int stile[D], sc[D];
     // Both loads are issued on every path (past the last tile their offsets
@@ -391,10 +416,7 @@ __global__ __launch_bounds__(64 * NW) void linear_split_kernel(
         }
     };
     // the ring's first chunks are in flight while W's image is built
-    load(SlotC<0>{});
-    load(SlotC<1>{});
-    load(SlotC<2>{});
-    load(SlotC<3>{});
+    each_slot<0, D>(load);
     {
         // one unit = one lane's operand granule of one (chunk, class tile):
         // 8 k of one class, split into its three pieces, stored side by side
@@ -592,10 +614,7 @@ __global__ __launch_bounds__(64 * NW) void linear_split_kernel(
         return true;
     };
     for (;;) {
-        if (!step(SlotC<0>{})) break;
-        if (!step(SlotC<1>{})) break;
-        if (!step(SlotC<2>{})) break;
-        if (!step(SlotC<3>{})) break;
+        if (!run_slots<0, D>(step)) break;
     }
     if constexpr (DIAG >= 2) {
         if (diag_sum == 12345.0f) Y[lane] = diag_sum;  // keeps the work live
