@@ -177,6 +177,15 @@ def _sync(X):
         torch.cuda.synchronize(X.device)
 
 
+def _align(X, group):
+    """A barrier through the group's own backend on X's device (a one-float
+    all-reduce, then a synchronise): no device guess as dist.barrier makes."""
+    dev = X.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.zeros(1, device=dev)
+    dist.all_reduce(t, group=group)
+    _sync(X)
+
+
 def _slowest(seconds, X, group):
     """Max over the group's ranks of each rank's seconds (list), one all-reduce."""
     dev = X.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
@@ -213,7 +222,7 @@ def precompute_group(csr, X, K, group):
     for c in cands:
         prop = _propagator(csr, group, c, staging)
         prop.propagate(X, K, output="replicated")
-        _sync(X)
+        _align(X, group)  # every rank starts the timed call together
         t0 = time.perf_counter()
         outs[c] = prop.propagate(X, K, output="replicated")
         _sync(X)
