@@ -96,6 +96,7 @@ class _LogitsCrossEntropy(torch.autograd.Function):
         return loss
 
     @staticmethod
+    @torch.autograd.function.once_differentiable  # (a double backward raises, never silently zero)
     def backward(ctx, grad_loss):
         from . import _lib
         logits, labels, lse, inv = ctx.saved_tensors
