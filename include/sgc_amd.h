@@ -337,8 +337,9 @@ int sgc_copy_blocks_f32(const float *src, int64_t lds, float *dst, int64_t ldd, 
  * tensor of the recorded shape, strides and alignment; each replayed launch
  * makes its kernel choice from the actual pointers, as a direct call does.
  * A list belongs to the device current at creation (the run switches to it
- * and back).  Not for concurrent runs of one list on different streams when
- * it holds fixed intermediates.  No reference counterpart: the reference's
+ * and back).  Runs, adds and destroys are serialised by one library lock
+ * (a run is a few launches); one list must still not run concurrently on
+ * two streams when it holds fixed intermediates.  No reference counterpart: the reference's
  * loop (utils.py:94-96) is one torch.spmm call per hop. */
 enum { SGC_SLOT_FIXED = 0, SGC_SLOT_X0 = 1, SGC_SLOT_OUT = 2 };
 int sgc_launch_list_create(int64_t *handle_host);

@@ -355,14 +355,13 @@ int sgc_launch_list_add_pad_rows(int64_t handle, const float *src, int64_t lds, 
 }
 
 int sgc_launch_list_run(int64_t handle, const float *X0, float *out, void *stream) {
-    const LaunchList *L = nullptr;
-    {
-        std::lock_guard<std::mutex> lock(g_lists_mu);
-        auto it = g_lists.find(handle);
-        SGC_REQUIRE(it != g_lists.end(), SGC_EINVAL, "launch_list_run: unknown handle %lld",
-                    (long long)handle);
-        L = &it->second;  // map nodes are stable; a list is not destroyed while it runs
-    }
+    // held for the whole run (a few launches): a concurrent destroy of this
+    // list from another thread waits instead of freeing it under the run
+    std::lock_guard<std::mutex> lock(g_lists_mu);
+    auto it = g_lists.find(handle);
+    SGC_REQUIRE(it != g_lists.end(), SGC_EINVAL, "launch_list_run: unknown handle %lld",
+                (long long)handle);
+    const LaunchList *L = &it->second;
     int cur = 0;
     hipError_t e = hipGetDevice(&cur);
     SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "launch_list_run: %s", hipGetErrorString(e));

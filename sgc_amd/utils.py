@@ -94,13 +94,15 @@ def sgc_precompute(features, adj, degree):
         t = perf_counter()
         return features, perf_counter() - t
     dev = features.device
-    if dev.type == "cuda":
-        _synchronize(dev)
+    if dev.type == "cuda" and not torch.cuda.current_stream(dev).query():
+        _synchronize(dev)  # earlier work on the caller's stream stays out of the time
     t = perf_counter()
     csr = csr_of(adj)
     out = _propagate_on_node(csr, features, degree)
     if dev.type == "cuda":
-        _synchronize(dev)
+        # every path joins its work (side streams, RCCL, other devices) back
+        # to the caller's stream, so that stream's completion is X_K's
+        torch.cuda.current_stream(dev).synchronize()
     return out, perf_counter() - t
 
 
