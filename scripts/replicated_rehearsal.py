@@ -47,7 +47,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from sgc_amd import graphs  # noqa: E402
-from sgc_amd.distributed import (REPLICATED_CHUNKS, FeaturePartitionedPropagator,  # noqa: E402
+from sgc_amd.distributed import (FeaturePartitionedPropagator,  # noqa: E402
                                  LinePartitionedPropagator, _copy_blocks, feature_bounds,
                                  line_bounds, make_shard, replicated_chunks)
 from sgc_amd.propagate import DeviceCSR, propagate  # noqa: E402
@@ -195,6 +195,9 @@ def main():
                          "FIRST_CHUNK_ALONE / HUB_EARLY); default: the product's")
     ap.add_argument("--breakdown", action="store_true",
                     help="time the replicated step without unpacks / in one chunk too")
+    ap.add_argument("--fractions", default="",
+                    help="semicolon-separated row fractions of the last hop's chunks to "
+                         "compare, e.g. 1,3,3,1;1,1,2,3,1 (sgc_amd.distributed.REPLICATED_CHUNKS)")
     ap.add_argument("--chunks", type=int, default=4,
                     help="last-hop chunks (4 = the product's 1:3:3:1 split, else equal)")
     args = ap.parse_args()
@@ -209,11 +212,16 @@ def main():
     import sgc_amd.distributed as D
     scheds = [dict(kv.split("=") for kv in part.split(",") if kv)
               for part in args.schedules.split(";")] if args.schedules else [{}]
-    for sched in scheds:
-        D.FIRST_CHUNK_ALONE = bool(int(sched.get("alone", int(D.FIRST_CHUNK_ALONE))))
-        D.HUB_EARLY = bool(int(sched.get("hub", int(D.HUB_EARLY))))
-        run_schedule(args, S, csr, X0, out, t1, F, K, n,
-                     {"alone": int(D.FIRST_CHUNK_ALONE), "hub": int(D.HUB_EARLY)})
+    fracs = ([tuple(int(v) for v in part.split(",")) for part in args.fractions.split(";")]
+             if args.fractions else [D.REPLICATED_CHUNKS])
+    for fr in fracs:
+        D.REPLICATED_CHUNKS = fr
+        for sched in scheds:
+            D.FIRST_CHUNK_ALONE = bool(int(sched.get("alone", int(D.FIRST_CHUNK_ALONE))))
+            D.HUB_EARLY = bool(int(sched.get("hub", int(D.HUB_EARLY))))
+            run_schedule(args, S, csr, X0, out, t1, F, K, n,
+                         {"alone": int(D.FIRST_CHUNK_ALONE), "hub": int(D.HUB_EARLY),
+                          "fractions": list(fr)})
 
 
 def run_schedule(args, S, csr, X0, out, t1, F, K, n, sched):
@@ -251,7 +259,8 @@ def run_schedule(args, S, csr, X0, out, t1, F, K, n, sched):
                 dst = torch.empty(nb, device="cuda")
                 step1, ready1 = timeline(prop, X0, K, args.reps, copy=(src, dst))
                 del src, dst
-                chunks = replicated_chunks(n, REPLICATED_CHUNKS if prop.chunks == 4
+                import sgc_amd.distributed as D
+                chunks = replicated_chunks(n, D.REPLICATED_CHUNKS if prop.chunks == 4
                                            else (1,) * prop.chunks)
                 gbytes = [(P - 1) * (r1 - r0) * wcols * 4 for r0, r1 in chunks]
                 # one chunk's unpack (the block-copy launch of P blocks)
