@@ -219,9 +219,10 @@ def main():
         for sched in scheds:
             D.FIRST_CHUNK_ALONE = bool(int(sched.get("alone", int(D.FIRST_CHUNK_ALONE))))
             D.HUB_EARLY = bool(int(sched.get("hub", int(D.HUB_EARLY))))
+            D.CHUNK_STREAMS = int(sched.get("streams", D.CHUNK_STREAMS))
             run_schedule(args, S, csr, X0, out, t1, F, K, n,
                          {"alone": int(D.FIRST_CHUNK_ALONE), "hub": int(D.HUB_EARLY),
-                          "fractions": list(fr)})
+                          "streams": D.CHUNK_STREAMS, "fractions": list(fr)})
 
 
 def run_schedule(args, S, csr, X0, out, t1, F, K, n, sched):

@@ -1175,15 +1175,21 @@ def _chunk_order(csr, chunks):
 #                     projection dropped (profiles/r05/rehearsal_sched.log).
 FIRST_CHUNK_ALONE = True
 HUB_EARLY = False
+# CHUNK_STREAMS      the chunks alternate between this many streams; 1 (in
+#                     order on one stream, each chunk alone on the GPU, so its
+#                     gather starts as early as it can): P = 8 lines 3.03x vs
+#                     2.95-3.00x on two (profiles/r05/rehearsal_streams.log).
+CHUNK_STREAMS = 1
 
 
 def _replicated_last_hop(prop, n, P, p, ld, X0, hop_into, gather, unpack):
     """The replicated output's last hop (feature and line partitions): in row
     chunks (replicated_chunks), each computed into this rank's slot of its
     chunk's [P*rows, ld] gather buffer and all-gathered in place as soon as it
-    is done; on the GPU the first chunk runs alone, the others alternate
-    between two streams (a chunk's launch does not wait for the previous
-    chunk's hub rows to join); with HUB_EARLY the hub rows of the chunk
+    is done; on the GPU the chunks run in order on one stream
+    (CHUNK_STREAMS; with two, the first alone and the others alternating, a
+    chunk's launch would not wait for the previous chunk's hub rows to join --
+    measured slower); with HUB_EARLY the hub rows of the chunk
     holding the longest row (the last one, _chunk_order) start at once on a
     third stream (measured slower: they delay the first chunk).
     Each gather is issued from its chunk's stream and waits for exactly that
@@ -1225,9 +1231,9 @@ def _replicated_last_hop(prop, n, P, p, ld, X0, hop_into, gather, unpack):
         full = prop._buf(("full", ci), (P * rows, ld), X0)
         loc = _gather_slot(full, p, rows)  # in-place gather: no copy of our block
         if gpu:
-            st = prop._chunk_streams[i % 2]
+            st = prop._chunk_streams[i % CHUNK_STREAMS]
             st.wait_stream(cur)
-            if first_done is not None and i % 2:
+            if first_done is not None and i % CHUNK_STREAMS:
                 st.wait_event(first_done)
             split = hub_split and i == len(order) - 1
             with torch.cuda.stream(st):
