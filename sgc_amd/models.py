@@ -131,6 +131,7 @@ def _cross_entropy_args(args, kwargs):
         return None
     if (x.dim() != 2 or x.dtype != torch.float32 or x.device.type != "cuda" or
             not 0 < x.shape[1] <= 64 or x.shape[0] == 0 or x.stride(1) != 1 or
+            x.stride(0) < x.shape[1] or
             y.dim() != 1 or y.dtype != torch.int64 or y.device != x.device or
             y.shape[0] != x.shape[0]):
         return None
