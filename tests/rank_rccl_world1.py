@@ -58,6 +58,25 @@ def main():
     torch.cuda.synchronize()
     rec["lines_replicated_equal"] = bool(torch.equal(got, want))
     rec["lines_sharded_equal"] = bool(torch.equal(sh, want))
+    # the product's 1:3:3:1 chunks and the measured-and-not-kept schedules of
+    # the replicated last hop (two alternating streams; the hub chunk's hub
+    # rows launched early on a third): the same bits
+    import sgc_amd.distributed as D
+    saved = (D.CHUNK_STREAMS, D.HUB_EARLY)
+    ok = True
+    try:
+        for streams, hub in ((1, False), (2, False), (2, True), (1, True)):
+            D.CHUNK_STREAMS, D.HUB_EARLY = streams, hub
+            for prop in (FeaturePartitionedPropagator(csr, chunks=4),
+                         LinePartitionedPropagator(make_shard(rp, ci, va, 0, 1, dev), csr=csr,
+                                                   chunks=4)):
+                prop.force_collectives = True
+                got = prop.propagate(X, 2, output="replicated")
+                torch.cuda.synchronize()
+                ok = ok and bool(torch.equal(got, want))
+    finally:
+        D.CHUNK_STREAMS, D.HUB_EARLY = saved
+    rec["schedules_equal"] = ok
     # the tail-stream pattern (LinePartitionedPropagator.propagate): gathers
     # issued from a side stream, waited there, then on the main stream
     full = [torch.zeros((64, 96), device=dev) for _ in range(2)]

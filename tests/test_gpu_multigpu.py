@@ -260,6 +260,7 @@ def test_rccl_exchange_paths_world1():
     assert rec["backend"] == "nccl" and rec["world"] == 1, rec
     assert rec["features_replicated_equal"] and rec["lines_replicated_equal"], rec
     assert rec["lines_sharded_equal"] and rec["tail_stream_pattern_ok"], rec
+    assert rec["schedules_equal"], rec  # 1:3:3:1 chunks, one / two streams, hub rows early
 
 
 def test_reddit_driver_runs_under_torchrun():
