@@ -240,3 +240,27 @@ def test_dropin_modules_reexport():
                 assert getattr(m, a).__module__.startswith("sgc_amd"), (name, a)
     finally:
         sys.path.pop(0)
+
+
+def test_cross_entropy_routing_rules():
+    """SGCLogits routes only the plain F.cross_entropy form to the HIP loss
+    (sgc_amd.models._cross_entropy_args): ROCm float32 [M, C <= 64] logits,
+    int64 [M] labels on the same device, mean reduction, no weights, no
+    smoothing; everything else -- CPU tensors here -- is torch's own call."""
+    import torch
+    from sgc_amd.models import SGCLogits, _cross_entropy_args
+    x = torch.randn(6, 5)
+    y = torch.randint(0, 5, (6,))
+    assert _cross_entropy_args((x, y), {}) is None  # CPU tensors: torch's path
+    ref = torch.nn.functional.cross_entropy(x, y)
+    got = torch.nn.functional.cross_entropy(x.as_subclass(SGCLogits), y)
+    assert type(got) is torch.Tensor and torch.equal(got, ref)
+    got = torch.nn.functional.cross_entropy(x.as_subclass(SGCLogits), y, reduction="sum")
+    assert torch.equal(got, torch.nn.functional.cross_entropy(x, y, reduction="sum"))
+    # non-plain forms are refused before any device check
+    for kw in ({"weight": torch.ones(5)}, {"reduction": "none"}, {"label_smoothing": 0.1},
+               {"size_average": False}, {"bogus": 1}):
+        assert _cross_entropy_args((x, y), kw) is None
+    assert _cross_entropy_args((x, y.to(torch.int32)), {}) is None
+    out = x.as_subclass(SGCLogits)
+    assert type(out.max(1)[1]) is torch.Tensor and type(out + 1) is torch.Tensor
