@@ -941,6 +941,36 @@ def test_prepared_loop_replay_bit_exact(tiny_cases, name, K):
     assert not lists()
 
 
+def test_launch_list_per_stream_and_release(tiny_cases):
+    """A launch list belongs to its stream: propagate() on a second stream
+    records its own (the intermediates are per stream), both replay the
+    reference's bits, and DeviceCSR.release_prepared() destroys them (the
+    next call records again)."""
+    from sgc_amd.propagate import DeviceCSR, propagate
+    c = tiny_cases["norm_n48_F602"]
+    csr = DeviceCSR.from_torch(coo_cuda(c))
+    X = torch.from_numpy(c["X"]).to(DEV)
+    lists = lambda: [k for k in csr._plans if isinstance(k, tuple) and k[0] == "list"]  # noqa: E731
+    side = torch.cuda.Stream()
+    outs = []
+    for _ in range(2):
+        outs.append(propagate(csr, X, 2))
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            outs.append(propagate(csr, X, 2))
+        torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert len(lists()) == 2
+    for o in outs:
+        assert bits_equal(o.cpu().numpy(), c["Y2"])
+    csr.release_prepared()
+    assert not lists()
+    again = propagate(csr, X, 2)
+    again = propagate(csr, X, 2)
+    torch.cuda.synchronize()
+    assert bits_equal(again.cpu().numpy(), c["Y2"]) and len(lists()) == 1
+
+
 def test_launch_list_abi_errors(tiny_cases):
     """sgc_launch_list_*: unknown handles, bad slots and a slot run without its
     pointer are errors (no launch); destroy frees the handle once; a list of
