@@ -1162,9 +1162,10 @@ def _chunk_order(csr, chunks):
 
 # Schedule of the replicated last hop's chunks (A/B knobs of
 # scripts/replicated_rehearsal.py; results never depend on them):
-#  FIRST_CHUNK_ALONE  the other chunks start after the first one, so its
-#                     gather (the link's first work) is not slowed by the
-#                     chunk beside it;
+#  FIRST_CHUNK_ALONE  with CHUNK_STREAMS > 1: the other chunks start after
+#                     the first one, so its gather (the link's first work) is
+#                     not slowed by the chunk beside it (on one stream every
+#                     chunk runs alone anyway);
 #  HUB_EARLY          the hub rows of the chunk holding the longest row run
 #                     early, on a stream of their own (with FIRST_CHUNK_ALONE:
 #                     from the first chunk's end on, beside the chunks after
