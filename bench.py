@@ -84,6 +84,35 @@ BASELINE_METRIC = ("propagated edges/sec (K-hop SpMM) + precompute wall-time, "
 SUB_STEPS = {"cora": (20, 5), "pubmed": (20, 5), "reddit": (10, 3), "rmat": (3, 1)}
 
 
+def output_check(shape, K, Y, seed):
+    """{"output_sha_ok": bool | None, ...}: SHA-256 of one timed call's X_K
+    against the hash the reference's own sgc_precompute produced for the
+    same seeded graph and features (tests/golden/shapes.json, written by
+    tests/golden/gen_golden.py).  None when no golden covers (shape, K, seed)."""
+    rec = {"output_sha_ok": None, "output_sha_basis": None}
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "shapes.json")) as f:
+            g = json.load(f).get(shape)
+    except (OSError, ValueError):
+        g = None
+    if not g or str(K) not in g.get("outputs", {}) or g.get("seed") != seed or \
+            g.get("feature_seed") != seed + 1:
+        rec["output_sha_basis"] = f"no golden for {shape} K={K} seed={seed}"
+        return rec
+    h = hashlib.sha256()
+    Yc = Y.detach()
+    rows = max(1, (256 << 20) // max(1, 4 * Yc.shape[1]))  # 256 MB host chunks
+    for r in range(0, Yc.shape[0], rows):
+        h.update(np.ascontiguousarray(Yc[r:r + rows].cpu().numpy()).tobytes())
+    got = h.hexdigest()
+    rec["output_sha_ok"] = got == g["outputs"][str(K)]["sha"]
+    rec["output_sha_basis"] = ("sha256 of the last timed call's X_K vs tests/golden/shapes.json "
+                               f"[{shape}][outputs][{K}] (the reference's sgc_precompute)")
+    if not rec["output_sha_ok"]:
+        rec["output_sha"] = got
+    return rec
+
+
 def gather_model_bytes(n, nnz, F):
     """row_ptr + (col, val) + one X row per nonzero + Y."""
     return 4 * (n + 1) + 8 * nnz + 4 * F * nnz + 4 * F * n
@@ -356,14 +385,18 @@ def single_gpu_shape(shape, args, dev, lib_sha, steps, warmup, S=None, X_host=No
     groups = prop_mod.column_groups_for(adj._sgc_amd_csr[1], F)
     launches = LaunchTimer(groups)
 
+    last = [None]
+
     def step():  # the public call, as the reference's drivers make it
-        return sgc_precompute(X0, adj, K)[0]
+        last[0] = sgc_precompute(X0, adj, K)[0]
 
     # value: the call as a caller sees it, nothing else in the loop; then the
     # same number of steps again with the library's per-launch events on (the
     # roofline's kernel times) -- at Cora shape those events alone would add
     # more host time per step than the two hops take on the GPU
     elapsed, _, _ = timed(step, steps, warmup, False, dev, events=False)
+    check = output_check(shape, K, last[0], args.seed)  # the last timed call's X_K
+    last[0] = None
     elapsed_i, step_ms, (hop_ms, light, hub, kernel) = timed(
         step, steps, 1, False, dev, on_start=launches.start, on_stop=launches.stop)
     hop_mean = float(np.mean(hop_ms))
@@ -386,6 +419,7 @@ def single_gpu_shape(shape, args, dev, lib_sha, steps, warmup, S=None, X_host=No
                                 kernel, groups, mean_or_none(launches.dispatch_light)),
            "hop_ms_median": float(np.median(hop_ms)),
            "timed_call": "sgc_precompute(features, adj, K) (sgc_amd.utils, the drop-in)"}
+    rec.update(check)
     del X0, adj
     torch.cuda.empty_cache()
     return rec, S, X_host
@@ -714,9 +748,18 @@ def main():
     partition = multigpu.partition_name(world)
     launches = LaunchTimer(1)
 
+    last = [None]
+
     def public_step():
-        return sgc_precompute(X0, adj, K)[0]
+        last[0] = sgc_precompute(X0, adj, K)[0]
     elapsed, _, _ = timed(public_step, args.steps, args.warmup, True, dev, events=False)
+    # every rank's X_K of the last timed call against the reference's hash
+    check = output_check(args.shape, K, last[0], args.seed)
+    last[0] = None
+    okv = torch.tensor([-1 if check["output_sha_ok"] is None else int(check["output_sha_ok"])],
+                       dtype=torch.int32, device=dev if args.dist_backend == "nccl" else "cpu")
+    dist.all_reduce(okv, op=dist.ReduceOp.MIN)
+    check["output_sha_ok_all_ranks"] = None if int(okv.item()) < 0 else bool(okv.item())
     # the same steps again with the library's per-launch events (rank 0's
     # launches: the roofline's kernel and times; label from the library)
     elapsed_i, step_ms, extra = timed(public_step, args.steps, 1, True, dev,
@@ -776,6 +819,7 @@ def main():
                     "first_call_seconds": round(first_pub, 4),
                     "loader_warmup_seconds": round(warm_s, 4),
                     "lib_sha256": lib_sha})
+        rec.update(check)
         if span:
             # rank 0's SpMM launches over one step: the compulsory bytes of its
             # K hops (S once, its block of X once, its Y once -- the same model

@@ -327,6 +327,41 @@ int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd,
 int sgc_copy_blocks_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int32_t nseg,
                         const int64_t *segs_host, void *stream);
 
+/* Peer exchange over IPC-mapped memory: the replicated output of the
+ * partitioned sgc_precompute (utils.py:92-97 returns all of X_K to every
+ * caller) without a gathered copy.  Each rank exposes one buffer of its own
+ * (its last hop's column blocks + int32 flags); the peers map it once and
+ * every call (1) computes a row chunk into that buffer, (2) raises the chunk's
+ * flag to the call's sequence number (sgc_signal_flag_i32), (3) waits for every
+ * peer's flag (sgc_wait_flags_i32) and (4) pulls all P blocks of the chunk
+ * straight into X_K's columns (sgc_pull_blocks_f32).
+ *
+ * sgc_ipc_get_handle: the SGC_IPC_HANDLE_BYTES handle of the allocation that
+ * holds `ptr` (hipIpcGetMemHandle) with ptr's offset in it.  sgc_ipc_open (in
+ * another process): maps it; *base_host is what sgc_ipc_close takes, *ptr_host
+ * the peer's pointer in this process. */
+#define SGC_IPC_HANDLE_BYTES 128
+int sgc_ipc_get_handle(const void *ptr, void *handle_host);
+int sgc_ipc_open(const void *handle_host, void **base_host, void **ptr_host);
+int sgc_ipc_close(void *base);
+/* *flag = value once everything enqueued on `stream` before it is visible at
+ * system scope (one-lane release store). */
+int sgc_signal_flag_i32(int32_t *flag, int32_t value, void *stream);
+/* The stream waits until flag_ptrs_host[i][0] >= value for every i < n (n <=
+ * 64; one polling wave, acquire loads at system scope); after timeout_us it
+ * stops waiting and sets *err = 1 (a host-visible word the caller checks after
+ * synchronising: a lost peer never hangs the device). */
+int sgc_wait_flags_i32(int32_t n, const int64_t *flag_ptrs_host, int32_t value, int32_t *err,
+                       int64_t timeout_us, void *stream);
+/* Batched 2-D block copy with one source pointer per segment (a peer's mapped
+ * buffer or this rank's own): segs_host[6s .. 6s+5] = (src pointer, src row
+ * stride in floats, dst_row, dst_col, rows, cols), nseg <= 16:
+ *     dst[dst_row + i, dst_col + j] = src[i * lds + j];
+ * sources read with system-coherent loads; a segment's source span must stay
+ * below 2 GiB (split its rows). */
+int sgc_pull_blocks_f32(int32_t nseg, const int64_t *segs_host, float *dst, int64_t ldd,
+                        void *stream);
+
 /* Recorded launch lists: the K-hop loop's launches (sgc_spmm_csr_f32_ex /
  * sgc_pad_rows_f32 with their arguments) recorded once and replayed by ONE
  * call per propagation -- at Pubmed shape the per-launch host cost (~4 us)

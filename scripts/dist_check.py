@@ -29,6 +29,33 @@ from sgc_amd import graphs  # noqa: E402
 from sgc_amd.distributed import RowPartitionedPropagator, TiledPropagator, make_shard  # noqa: E402
 
 
+def _sha(t):
+    return hashlib.sha256(t.cpu().numpy().tobytes()).hexdigest()
+
+
+def replicated_checks(prop, X, K, g):
+    """The replicated output on this rank -- every rank's full X_K -- through
+    the default exchange on the GPU (IPC pulls of the peers' blocks, no
+    gathered copy) and through the collective one (in-place all-gathers +
+    unpack): both against the reference's hash.  Then three IPC calls with
+    X, 2X and 4X: S^K (2^j X) = 2^j S^K X bit for bit (power-of-two scaling
+    is exact through every fma), and the calls alternate the window's two
+    halves, so a block left over from an earlier call would show."""
+    want = g["outputs"][str(K)]["sha"]
+    os.environ["SGC_AMD_REPLICATED_EXCHANGE"] = "collective"
+    coll = prop.propagate(X, K, output="replicated")
+    rec = {"collective_sha_ok": _sha(coll) == want}
+    del coll
+    os.environ.pop("SGC_AMD_REPLICATED_EXCHANGE")
+    outs = [prop.propagate(X * float(2 ** j), K, output="replicated") for j in range(3)]
+    torch.cuda.synchronize()
+    rec["default_sha_ok"] = _sha(outs[0]) == want
+    rec["scaled_calls_exact"] = all(torch.equal(outs[j], outs[0] * float(2 ** j)) for j in (1, 2))
+    rec["exchange"] = "ipc" if getattr(prop, "_ipc", None) is not None else "collective"
+    rec["ipc_unavailable"] = getattr(prop, "ipc_unavailable", None) or ""
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shape", default="reddit")
@@ -42,7 +69,8 @@ def main():
                     help="features: the sharded exchange")
     ap.add_argument("--pieces", type=int, default=None, help="features: pairwise row pieces")
     ap.add_argument("--also-replicated", action="store_true",
-                    help="lines: also check the replicated output against the sharded rows")
+                    help="lines / features: also check the replicated output (IPC and "
+                         "collective exchanges) against the reference hash")
     ap.add_argument("--device", default="cuda", help="cpu: the CPU-twin rehearsal")
     ap.add_argument("--cache", default=os.environ.get("TMPDIR", "/tmp"))
     args = ap.parse_args()
@@ -77,6 +105,7 @@ def main():
     del Xh
     K = spec["hops"]
     row_index = None
+    replicated = None
     if args.partition == "cyclic":
         from sgc_amd.distributed import CyclicRowPropagator
         cp = CyclicRowPropagator(S.row_ptr, S.col_idx, S.val, rank, world, dev, tile=args.tile,
@@ -92,6 +121,8 @@ def main():
         fp = FeaturePartitionedPropagator(csr, host_staging=True, exchange=args.exchange,
                                           pieces=args.pieces)
         mine = fp.propagate(X, K, output="sharded")
+        if args.also_replicated:
+            replicated = replicated_checks(fp, X, K, g)
         rb = equal_row_bounds(g["n"], world)
         r0, r1 = int(rb[rank]), int(rb[rank + 1])
     elif args.partition == "lines":
@@ -103,6 +134,7 @@ def main():
         lp = LinePartitionedPropagator(shard, csr=csr, host_staging=True)
         mine = lp.propagate(X, K, output="sharded")
         if args.also_replicated:  # every rank's full X_K must equal the sharded rows
+            replicated = replicated_checks(lp, X, K, g)
             full = lp.propagate(X, K, output="replicated")
             rb = equal_row_bounds(g["n"], world)
             assert torch.equal(full[int(rb[rank]):int(rb[rank + 1])], mine)
@@ -124,6 +156,8 @@ def main():
         torch.cuda.synchronize()
     blocks = [None] * world if rank == 0 else None
     dist.gather_object((r0, r1, row_index, mine.cpu().numpy()), blocks, dst=0)
+    reps = [None] * world if rank == 0 else None
+    dist.gather_object(replicated, reps, dst=0)
     if rank == 0:
         Y = np.empty((g["n"], g["features"]), np.float32)
         covered = np.zeros(g["n"], bool)
@@ -144,6 +178,11 @@ def main():
                           "rows_per_rank": [int(b - a) if ri is None else int(len(ri))
                                             for a, b, ri, _ in blocks],
                           "bit_exact_vs_reference_hash": ok,
+                          "replicated": None if replicated is None else {
+                              k: all(r[k] for r in reps) for k in replicated
+                              if isinstance(replicated[k], bool)},
+                          "replicated_exchange": None if replicated is None else
+                              sorted({r["exchange"] for r in reps}),
                           "seconds": round(time.time() - t0, 1)}), flush=True)
     dist.barrier()
     dist.destroy_process_group()

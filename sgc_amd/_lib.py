@@ -53,6 +53,12 @@ SIGNATURES = {
                                                  _i32, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "sgc_pad_rows_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i64, _p]),
     "sgc_copy_blocks_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i32, _p, _p]),
+    "sgc_ipc_get_handle": (ctypes.c_int, [_p, _p]),
+    "sgc_ipc_open": (ctypes.c_int, [_p, ctypes.POINTER(_p), ctypes.POINTER(_p)]),
+    "sgc_ipc_close": (ctypes.c_int, [_p]),
+    "sgc_signal_flag_i32": (ctypes.c_int, [_p, _i32, _p]),
+    "sgc_wait_flags_i32": (ctypes.c_int, [_i32, _p, _i32, _p, _i64, _p]),
+    "sgc_pull_blocks_f32": (ctypes.c_int, [_i32, _p, _p, _i64, _p]),
     "sgc_aligned_ld": (_i64, [_i64]),
     "sgc_launch_list_create": (ctypes.c_int, [ctypes.POINTER(_i64)]),
     "sgc_launch_list_add_spmm": (ctypes.c_int, [_i64, _p, _p, _p, _i64, _i64, _p, _i64, _p, _i64,

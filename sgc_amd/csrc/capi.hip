@@ -39,6 +39,14 @@ int launch_pad_rows(const float *src, int64_t lds, float *dst, int64_t ldd, int6
                     int64_t F, hipStream_t stream);
 int launch_copy_blocks(const float *src, int64_t lds, float *dst, int64_t ldd, int32_t nseg,
                        const int64_t *segs, hipStream_t stream);
+int launch_pull_blocks(int32_t nseg, const int64_t *segs, float *dst, int64_t ldd,
+                       hipStream_t stream);
+int launch_wait_flags(int32_t n, const int64_t *flags, int32_t value, int32_t *err,
+                      int64_t timeout_us, hipStream_t stream);
+int launch_signal_flag(int32_t *flag, int32_t value, hipStream_t stream);
+int ipc_get_handle(const void *ptr, void *handle);
+int ipc_open(const void *handle, void **base, void **ptr);
+int ipc_close(void *base);
 size_t augnorm_scan_temp_bytes(int64_t n);
 int augnorm_count(const int32_t *row_ptr, const int32_t *col, const double *val, int64_t n,
                   int64_t nnz, int32_t *out_row_ptr, double *rowsum, void *ws, size_t ws_bytes,
@@ -252,6 +260,28 @@ int sgc_pad_rows_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int
 int sgc_copy_blocks_f32(const float *src, int64_t lds, float *dst, int64_t ldd, int32_t nseg,
                         const int64_t *segs_host, void *stream) {
     return launch_copy_blocks(src, lds, dst, ldd, nseg, segs_host, as_stream(stream));
+}
+
+int sgc_ipc_get_handle(const void *ptr, void *handle_host) { return ipc_get_handle(ptr, handle_host); }
+
+int sgc_ipc_open(const void *handle_host, void **base_host, void **ptr_host) {
+    return ipc_open(handle_host, base_host, ptr_host);
+}
+
+int sgc_ipc_close(void *base) { return ipc_close(base); }
+
+int sgc_signal_flag_i32(int32_t *flag, int32_t value, void *stream) {
+    return launch_signal_flag(flag, value, as_stream(stream));
+}
+
+int sgc_wait_flags_i32(int32_t n, const int64_t *flag_ptrs_host, int32_t value, int32_t *err,
+                       int64_t timeout_us, void *stream) {
+    return launch_wait_flags(n, flag_ptrs_host, value, err, timeout_us, as_stream(stream));
+}
+
+int sgc_pull_blocks_f32(int32_t nseg, const int64_t *segs_host, float *dst, int64_t ldd,
+                        void *stream) {
+    return launch_pull_blocks(nseg, segs_host, dst, ldd, as_stream(stream));
 }
 
 // Recorded launch lists (sgc_launch_list_*): the K-hop loop's launches built

@@ -205,6 +205,42 @@ def make_shard(row_ptr, col_idx, val, rank, world_size, device, balance="nnz"):
                     t(np.asarray(val[k0:k1]), torch.float32), int(row_ptr.shape[0] - 1), cg)
 
 
+def make_shard_device(csr, rank, world_size, balance="nnz"):
+    """make_shard for a DeviceCSR without a host round trip: the row bounds
+    from a searchsorted over the device row_ptr (P+1 ints come back), the
+    rank's col_idx / val as views of the adjacency's own arrays (no copy),
+    its row_ptr rebased and its gathered column ids computed on the device.
+    The same ShardCSR as make_shard(host arrays) -- tests compare them."""
+    rp = csr.row_ptr
+    n, nnz = int(csr.n_rows), int(csr.nnz)
+    if balance == "nnz":
+        targets = (torch.arange(1, world_size, dtype=torch.float64) * nnz / world_size)
+        # searchsorted(side="left") of float targets over the int row_ptr,
+        # as nnz_balanced_bounds: the first row whose start is >= target
+        tgt = torch.ceil(targets).to(torch.int64).to(rp.device)
+        inner = torch.searchsorted(rp.to(torch.int64), tgt, right=False).clamp(0, n).cpu()
+        bounds = np.concatenate([[0], inner.numpy(), [n]]).astype(np.int64)
+    else:
+        bounds = partition_bounds(np.zeros(n + 1, np.int64), world_size, balance)
+    B = max(1, int(np.max(np.diff(bounds))))
+    if world_size * B >= 2**31:
+        raise ValueError("gathered exchange buffer exceeds int32 row ids")
+    r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
+    ks = rp[[r0, r1]].cpu()
+    k0, k1 = int(ks[0]), int(ks[1])
+    cols = csr.col_idx[k0:k1]
+    vals = csr.val[k0:k1]
+    row_ptr = (rp[r0:r1 + 1] - k0).to(torch.int32)
+    if all(int(bounds[p]) == min(p * B, n) for p in range(world_size + 1)):
+        cg = cols  # equal blocks: gathered row j is node j
+    else:
+        b = torch.as_tensor(bounds, dtype=torch.int64, device=cols.device)
+        j = cols.to(torch.int64)
+        q = torch.searchsorted(b, j, right=True) - 1
+        cg = (j - b[q] + q * B).to(torch.int32)
+    return ShardCSR(rank, world_size, bounds, row_ptr, cols, vals, n, cg)
+
+
 def _default_spmm(shard: ShardCSR, X, out, layout="input", part="all", rows=None):
     """This rank's rows of S.X through the product engine (HIP on ROCm
     tensors, the CPU twin on CPU tensors).  layout: "input" = X is the
@@ -1150,11 +1186,11 @@ def _chunk_order(csr, chunks):
     key = ("chunk_order", tuple(chunks))
     order = csr._plans.get(key)
     if order is None:
-        rp = csr._plans.get(("host_row_ptr",))
-        if rp is None:
-            rp = csr._plans[("host_row_ptr",)] = np.asarray(csr.row_ptr.cpu(), dtype=np.int64)
-        deg = np.diff(rp)
-        longest = [int(deg[r0:r1].max()) if r1 > r0 else 0 for r0, r1 in chunks]
+        # each chunk's longest row, on the adjacency's device (len(chunks)
+        # ints come back, not the row_ptr)
+        deg = csr.row_ptr[1:] - csr.row_ptr[:-1]
+        longest = torch.stack([deg[r0:r1].max() if r1 > r0 else deg.new_zeros(())
+                               for r0, r1 in chunks]).cpu().tolist()
         hub = int(np.argmax(longest))
         order = csr._plans[key] = [c for c in range(len(chunks)) if c != hub] + [hub]
     return order
@@ -1259,6 +1295,213 @@ def _replicated_last_hop(prop, n, P, p, ld, X0, hop_into, gather, unpack):
         unpack(full, r0, r1)
 
 
+# ---------------------------------------------------------------------------
+# The replicated last hop over IPC-mapped peer memory (no gathered copy).
+
+IPC_TIMEOUT_US = 20_000_000  # a peer silent this long: the call raises
+IPC_FLAG_WORDS = 64          # int32 flags after the two halves: chunk c ready = word c,
+IPC_DONE = 32                # this rank's pulls of a call done = word 32
+
+
+def replicated_exchange_mode(X0, world, force=False):
+    """How the feature / line partitions hand out the replicated X_K:
+    "ipc" (peers' blocks pulled straight into X_K's columns) on the GPU with
+    more than one rank, else "collective" (in-place all-gather + unpack);
+    SGC_AMD_REPLICATED_EXCHANGE=ipc|collective forces one."""
+    import os
+    m = os.environ.get("SGC_AMD_REPLICATED_EXCHANGE", "auto")
+    if m not in ("auto", "ipc", "collective"):
+        raise ValueError("SGC_AMD_REPLICATED_EXCHANGE must be auto, ipc or collective, "
+                         f"not {m!r}")
+    if not X0.is_cuda:
+        return "collective"
+    if m == "auto":
+        return "ipc" if (world > 1 or force) else "collective"
+    return m
+
+
+class IpcPeers:
+    """One rank's window for the replicated last hop, mapped by every peer.
+
+    The window is one allocation: two [n, ld] fp32 halves (call s writes half
+    s & 1, so a slow peer still reading call s-1's blocks is never
+    overwritten; before writing half h again a rank waits for every peer's
+    `done` flag of call s-2) and IPC_FLAG_WORDS int32 flags.  The handles are
+    exchanged once through the process group (all_gather_object: gloo or
+    RCCL), each peer's window opened with sgc_ipc_open (hipIpcOpenMemHandle:
+    another GPU over xGMI, or the same GPU from another process in the
+    one-GPU rehearsal).  `err` is a pinned host word the wait kernels set when
+    a peer stays silent for IPC_TIMEOUT_US."""
+
+    def __init__(self, group, rank, world, n, ld, device):
+        import ctypes
+        from . import _lib
+        lib = _lib.load()
+        self.rank, self.world, self.n, self.ld = rank, world, int(n), int(ld)
+        half = self.n * self.ld
+        self.window = torch.empty(2 * half + IPC_FLAG_WORDS, dtype=torch.float32, device=device)
+        self.flags = self.window[2 * half:].view(torch.int32)
+        self.flags.zero_()
+        self.halves = [self.window[:half].view(self.n, self.ld),
+                       self.window[half:2 * half].view(self.n, self.ld)]
+        self.err = torch.zeros(1, dtype=torch.int32).pin_memory()
+        torch.cuda.synchronize(device)  # zeroed flags before any peer reads them
+        h = ctypes.create_string_buffer(128)
+        _lib.check(lib.sgc_ipc_get_handle(_lib.ptr(self.window), h), "ipc_get_handle")
+        handles = [None] * world
+        dist.all_gather_object(handles, h.raw, group=group)
+        self.ptrs, self._bases = [], []
+        try:
+            for q in range(world):
+                if q == rank:
+                    self.ptrs.append(self.window.data_ptr())
+                    continue
+                base, ptr = ctypes.c_void_p(), ctypes.c_void_p()
+                buf = ctypes.create_string_buffer(handles[q], 128)
+                with torch.cuda.device(device):
+                    _lib.check(lib.sgc_ipc_open(buf, ctypes.byref(base), ctypes.byref(ptr)),
+                               "ipc_open")
+                self._bases.append(base.value)
+                self.ptrs.append(ptr.value)
+        except Exception:
+            self.close()
+            raise
+        self.seq = 0
+
+    def half_ptr(self, q, h, row=0):
+        return self.ptrs[q] + 4 * (h * self.n * self.ld + row * self.ld)
+
+    def flag_ptr(self, q, word):
+        return self.ptrs[q] + 4 * (2 * self.n * self.ld + word)
+
+    def close(self):
+        from . import _lib
+        for b in self._bases:
+            try:
+                _lib.load().sgc_ipc_close(b)
+            except Exception:  # interpreter shutdown
+                pass
+        self._bases = []
+
+    def __del__(self):
+        self.close()
+
+    def signal(self, word, value, stream):
+        from . import _lib
+        _lib.check(_lib.load().sgc_signal_flag_i32(
+            ctypes_void(self.flag_ptr(self.rank, word)), int(value),
+            ctypes_void(stream.cuda_stream)), "signal_flag_i32")
+
+    def wait(self, word, value, stream, ranks=None):
+        import ctypes
+        from . import _lib
+        ranks = range(self.world) if ranks is None else list(ranks)
+        ptrs = [self.flag_ptr(q, word) for q in ranks]
+        if not ptrs:
+            return
+        arr = (ctypes.c_int64 * len(ptrs))(*ptrs)
+        _lib.check(_lib.load().sgc_wait_flags_i32(len(ptrs), arr, int(value),
+                                                  ctypes_void(self.err.data_ptr()),
+                                                  IPC_TIMEOUT_US,
+                                                  ctypes_void(stream.cuda_stream)),
+                   "wait_flags_i32")
+
+    def check(self, stream):
+        """After the caller's stream is done: raise if a wait timed out."""
+        stream.synchronize()
+        if int(self.err[0]) != 0:
+            self.err.zero_()
+            raise RuntimeError("sgc_amd: a peer's block of the replicated X_K never became "
+                               f"ready within {IPC_TIMEOUT_US / 1e6:.0f} s (IPC exchange)")
+
+
+def ctypes_void(v):
+    import ctypes
+    return ctypes.c_void_p(int(v))
+
+
+def _ipc_for(prop, group, rank, world, n, ld, device):
+    """The propagator's IpcPeers window for [n, ld] halves, made once
+    (collective: every rank builds it in the same call); None when a rank
+    could not map its peers -- then every rank keeps the collective path."""
+    key = (n, ld, str(device))
+    if getattr(prop, "_ipc_key", None) == key:
+        return prop._ipc
+    ok, ipc, why = 1, None, ""
+    try:
+        ipc = IpcPeers(group, rank, world, n, ld, device)
+    except Exception as e:  # noqa: BLE001 -- recorded, agreed on below
+        ok, why = 0, f"{type(e).__name__}: {e}"
+    if world > 1:
+        dev = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        t = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        ok = int(t.item())
+    if not ok:
+        if ipc is not None:
+            ipc.close()
+        ipc = None
+        prop.ipc_unavailable = why or "a peer could not map the windows"
+    prop._ipc, prop._ipc_key = ipc, key
+    return ipc
+
+
+def _replicated_last_hop_ipc(prop, ipc, n, P, p, X0, hop_into, blocks, out):
+    """The replicated output's last hop through IpcPeers: the rows in the
+    chunks and order of _replicated_last_hop, each computed into this rank's
+    half of its window on the chunk stream and announced by a flag; the
+    caller's stream then, per chunk, waits for its own event and every
+    peer's flag and pulls all P column blocks (blocks[q] = (col0, width) of
+    rank q in X_K) straight into `out` -- one sgc_pull_blocks_f32 launch per
+    chunk, no gather buffer, no unpack.  Bit-identical: the bytes are moved,
+    never recomputed."""
+    import ctypes
+    from . import _lib
+    lib = _lib.load()
+    ipc.seq += 1
+    seq, h = ipc.seq, ipc.seq & 1
+    mine = ipc.halves[h]
+    cur = torch.cuda.current_stream(X0.device)
+    if getattr(prop, "_chunk_streams", None) is None or \
+            prop._chunk_streams[0].device != X0.device:
+        prop._chunk_streams = [torch.cuda.Stream(X0.device) for _ in range(3)]
+    st = prop._chunk_streams[0]
+    st.wait_stream(cur)
+    chunks = replicated_chunks(n, REPLICATED_CHUNKS if prop.chunks == 4 else (1,) * prop.chunks)
+    order = _chunk_order(getattr(prop, "csr", None), chunks)
+    if len(order) > 32:
+        raise ValueError("IPC exchange: at most 32 chunks")
+    evs = []
+    with torch.cuda.stream(st):
+        if seq > 2:  # every peer is done reading this half (call seq - 2)
+            ipc.wait(IPC_DONE, seq - 2, st, ranks=[q for q in range(P) if q != p])
+        for ci in order:
+            r0, r1 = chunks[ci]
+            hop_into(r0, r1, mine[r0:r1])
+            ipc.signal(ci, seq, st)
+            ev = torch.cuda.Event()
+            ev.record(st)
+            evs.append(ev)
+    max_rows = max(1, ((1 << 31) - 1) // (4 * ipc.ld) - 1)  # a segment's span < 2 GiB
+    for ci, ev in zip(order, evs):
+        r0, r1 = chunks[ci]
+        cur.wait_event(ev)
+        ipc.wait(ci, seq, cur, ranks=[q for q in range(P) if q != p])
+        segs = []
+        for a in range(r0, r1, max_rows):
+            b = min(r1, a + max_rows)
+            for q in range(P):
+                c0, w = blocks[q]
+                if w > 0:
+                    segs.append((ipc.half_ptr(q, h, a), ipc.ld, a, c0, b - a, w))
+        for i in range(0, len(segs), 16):
+            part = segs[i:i + 16]
+            arr = (ctypes.c_int64 * (6 * len(part)))(*[v for sg in part for v in sg])
+            _lib.check(lib.sgc_pull_blocks_f32(len(part), arr, _lib.ptr(out), out.stride(0),
+                                               ctypes_void(cur.cuda_stream)), "pull_blocks_f32")
+    ipc.signal(IPC_DONE, seq, cur)
+
+
 def _gather_slot(full, p, rows):
     """Rank p's slot of an all-gather buffer [P*rows, ld]: the last hop writes
     its rows there and the gather runs in place (NCCL/RCCL in-place
@@ -1339,6 +1582,10 @@ class FeaturePartitionedPropagator:
     # calls -- async all-gathers from a side stream, in-place slots, waits
     # across streams -- that P > 1 runs
     force_collectives = False
+    # test hook: the replicated last hop through the IPC window at world 1
+    # (its own block pulled by sgc_pull_blocks_f32, flags signalled/awaited)
+    force_ipc = False
+    ipc_unavailable = None  # why the IPC window could not be mapped, if so
 
     def _buf(self, key, shape, like):
         b = self._bufs.get(key)
@@ -1475,8 +1722,8 @@ class FeaturePartitionedPropagator:
             if w and n:
                 hop(src, 0, n, dst, own, True)
             src, own = dst, True
-        if P == 1 and not self.force_collectives:  # the last hop writes X_K itself
-            if w and n:
+        if P == 1 and not (self.force_collectives or self.force_ipc):
+            if w and n:  # the last hop writes X_K itself
                 hop(src, 0, n, out, own, False)
             return out
         if output == "sharded" and (self.exchange == "pairwise" or
@@ -1506,6 +1753,14 @@ class FeaturePartitionedPropagator:
         def hop_into(r0, r1, loc, flags=0):
             if w:
                 hop(src, r0, r1, loc[:, :w], own, True, flags)
+
+        if replicated_exchange_mode(X0, P, self.force_ipc) == "ipc":
+            ipc = _ipc_for(self, self.group, p, P, n, ld, X0.device)
+            if ipc is not None:
+                blocks = [(int(bounds[q]), int(bounds[q + 1] - bounds[q])) for q in range(P)]
+                _replicated_last_hop_ipc(self, ipc, n, P, p, X0, hop_into, blocks, out)
+                ipc.check(torch.cuda.current_stream(X0.device))
+                return out
 
         def unpack(full, r0, r1):
             rows = r1 - r0
@@ -1603,7 +1858,9 @@ class LinePartitionedPropagator:
             self._tail_stream = torch.cuda.Stream(device)
         return torch.cuda.stream(self._tail_stream)
 
-    force_collectives = False  # test hook, as FeaturePartitionedPropagator's
+    force_collectives = False  # test hooks, as FeaturePartitionedPropagator's
+    force_ipc = False
+    ipc_unavailable = None
 
     def _collective(self, kind, dst, src):
         if self.world_size == 1 and not self.force_collectives:
@@ -1716,11 +1973,14 @@ class LinePartitionedPropagator:
         if wt:  # the tail of X_K from the last gather
             r0, r1 = (0, n) if output == "replicated" else (int(rb[p]), int(rb[p + 1]))
             self._tail_rows(full, wt, r0, r1, out[:, T:F])
+        ipc, self._ipc_pending = getattr(self, "_ipc_pending", None), None
+        if ipc is not None:
+            ipc.check(torch.cuda.current_stream(X0.device))
         return out
 
     def _last_replicated(self, msrc, mown, out, main_hop, W, w, ld, P, X0):
         n, F = out.shape
-        if P == 1 and not self.force_collectives:
+        if P == 1 and not (self.force_collectives or self.force_ipc):
             if w and n:
                 main_hop(msrc, 0, n, out[:, :w], mown, False)
             return
@@ -1729,6 +1989,14 @@ class LinePartitionedPropagator:
         def hop_into(r0, r1, loc, flags=0):
             if w:
                 main_hop(msrc, r0, r1, loc[:, :w], mown, True, flags)
+
+        if replicated_exchange_mode(X0, P, self.force_ipc) == "ipc":
+            ipc = _ipc_for(self, self.group, self.rank, P, n, ld, X0.device)
+            if ipc is not None:
+                blocks = [(min(q * W, F), min((q + 1) * W, F) - min(q * W, F)) for q in range(P)]
+                _replicated_last_hop_ipc(self, ipc, n, P, self.rank, X0, hop_into, blocks, out)
+                self._ipc_pending = ipc
+                return
 
         def unpack(full, r0, r1):
             rows = r1 - r0

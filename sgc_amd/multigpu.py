@@ -42,10 +42,14 @@ import time
 import torch
 import torch.distributed as dist
 
-PARTITIONS = ("auto", "replicate", "features", "lines", "rows", "cyclic")
-# what "auto" times on the first call (the row and cyclic partitions move X_k
-# after every hop: never faster for a replicated X_K)
+PARTITIONS = ("auto", "tune", "replicate", "features", "lines", "rows", "cyclic")
+# what "tune" times (the row and cyclic partitions move X_k after every hop:
+# never faster for a replicated X_K)
 AUTO_CANDIDATES = ("replicate", "features", "lines")
+# below this much work (nnz(S) * F multiply-adds per hop) a call is a few
+# hundred microseconds on one GPU and the exchange's latency would eat any
+# split: "auto" replicates.  Pubmed shape: 5.4e7; Reddit shape: 1.4e10.
+AUTO_MIN_WORK = 1 << 30
 
 
 def torchrun_env():
@@ -107,13 +111,91 @@ def process_group(device):
 
 
 def partition_name(world=None):
-    """The partition SGC_AMD_PARTITION names ("auto", the default, is chosen
-    by measured time on the first call: precompute_group).  `world` is
-    accepted for the callers that pass it; it does not change the name."""
+    """The partition SGC_AMD_PARTITION names ("auto", the default: a persisted
+    per-node choice when one exists, else rule_choice -- one propagation on
+    the first call, no trials; "tune": the same first call, candidates timed
+    on the second; precompute_group).  `world` is accepted for the callers
+    that pass it; it does not change the name."""
     p = os.environ.get("SGC_AMD_PARTITION", "auto")
     if p not in PARTITIONS:
         raise ValueError(f"SGC_AMD_PARTITION must be one of {PARTITIONS}, not {p!r}")
     return p
+
+
+def rule_choice(world, n, nnz, F, K):
+    """The partition "auto" uses without a persisted choice, from the one-GPU
+    rehearsal of every candidate at Reddit shape: at P = 2
+    replicating beats both splits (the one link carries half of X_K: features
+    0.95-0.97x, lines 0.88-0.92x), at P >= 3 the line partition leads (P = 4
+    1.85x, P = 8 2.8-3.1x; features 1.6x / 2.8-2.9x), provided each rank owns
+    at least one whole 128-B line (F >= 32 P), else features; calls with less
+    than AUTO_MIN_WORK multiply-adds per hop replicate (they are latency-bound
+    on one GPU).  Identical on every rank: no collective."""
+    min_work = int(os.environ.get("SGC_AMD_AUTO_MIN_WORK", AUTO_MIN_WORK))
+    if world <= 2 or K <= 0 or int(nnz) * int(F) < min_work:
+        return "replicate"
+    from .distributed import line_bounds
+    W, _ = line_bounds(int(F), int(world))
+    return "lines" if W > 0 else "features"
+
+
+def _lib_sha():
+    """sha256 of the loaded libsgc_amd.so (part of a persisted choice's key:
+    a new library may change which candidate wins)."""
+    import hashlib
+    from . import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def tune_file():
+    """Where "tune" persists its measured choices (one JSON object per node):
+    SGC_AMD_TUNE_FILE, default ~/.cache/sgc_amd/partitions.json."""
+    return os.environ.get("SGC_AMD_TUNE_FILE") or os.path.join(
+        os.path.expanduser("~"), ".cache", "sgc_amd", "partitions.json")
+
+
+def _tune_key(world, n, nnz, F, K, device):
+    name = torch.cuda.get_device_name(device) if device.type == "cuda" else "cpu"
+    return f"world={world} n={n} nnz={nnz} F={F} K={K} dev={name} lib={_lib_sha()[:16]}"
+
+
+def persisted_choice(world, n, nnz, F, K, device):
+    """A choice "tune" measured earlier on this node for exactly this
+    (world, n, nnz, F, K, device model, library), or None."""
+    path = tune_file()
+    if not os.path.exists(path):
+        return None
+    import json
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(_tune_key(world, n, nnz, F, K, device))
+    except (OSError, ValueError):
+        return None
+    c = rec.get("chosen") if isinstance(rec, dict) else None
+    return c if c in AUTO_CANDIDATES else None
+
+
+def _persist_choice(world, n, nnz, F, K, device, chosen, seconds):
+    import json
+    path = tune_file()
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            d = {}
+        d[_tune_key(world, n, nnz, F, K, device)] = {"chosen": chosen, "seconds": seconds}
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
+            json.dump(d, f, indent=1, sort_keys=True)
+        os.replace(tmp, path)
+    except OSError:
+        pass  # a read-only home: the choice is kept for this process only
 
 
 def _host_csr(csr):
@@ -129,7 +211,8 @@ def _propagator(csr, group, partition, staging):
     """The partitioned propagator for (adjacency, group, partition), built once
     and cached on the adjacency's CSR with its buffers and prepared launches."""
     from .distributed import (CyclicRowPropagator, FeaturePartitionedPropagator,
-                              LinePartitionedPropagator, RowPartitionedPropagator, make_shard)
+                              LinePartitionedPropagator, RowPartitionedPropagator,
+                              make_shard_device)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     key = ("dist", id(group), rank, world, partition, staging)
     prop = csr._plans.get(key)
@@ -141,12 +224,10 @@ def _propagator(csr, group, partition, staging):
         prop = FeaturePartitionedPropagator(csr, rank=rank, world_size=world, group=group,
                                             host_staging=staging)
     elif partition == "lines":
-        rp, ci, va = _host_csr(csr)
-        shard = make_shard(rp, ci, va, rank, world, csr.device)
+        shard = make_shard_device(csr, rank, world)  # no host copy of S
         prop = LinePartitionedPropagator(shard, csr=csr, group=group, host_staging=staging)
     elif partition == "rows":
-        rp, ci, va = _host_csr(csr)
-        shard = make_shard(rp, ci, va, rank, world, csr.device)
+        shard = make_shard_device(csr, rank, world)
         prop = RowPartitionedPropagator(shard, group=group, host_staging=staging)
     else:
         rp, ci, va = _host_csr(csr)
@@ -196,41 +277,95 @@ def _slowest(seconds, X, group):
 
 def auto_choice(csr, group, F, K):
     """The auto partition's record for (adjacency, group, F, K) once chosen:
-    {"chosen": name, "seconds": {candidate: slowest rank's time}}, or None."""
+    {"chosen": name, "how": "rule" | "persisted" | "timed", "seconds":
+    {candidate: slowest rank's time} (timed only)}, or None."""
     return csr._plans.get(("auto", id(group), dist.get_world_size(group), int(F), int(K)))
+
+
+# how many partitioned propagations precompute_group ran (tests: the first
+# call of "auto" / "tune" runs exactly one)
+PROPAGATIONS = [0]
+
+
+def _run(prop, X, K):
+    PROPAGATIONS[0] += 1
+    return prop.propagate(X, K, output="replicated")
+
+
+def _drop_propagator(csr, group, name, staging):
+    """Forget a candidate's propagator and its buffers (a tuned loser)."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    prop = csr._plans.pop(("dist", id(group), rank, world, name, staging), None)
+    if prop is not None and hasattr(prop, "release"):
+        prop.release()
 
 
 def precompute_group(csr, X, K, group):
     """X_K = S^K X on every rank of `group`, partitioned (the caller has
     checked shapes and devices).  Collective: every rank must call it with
-    the same adjacency and feature shape (the auto choice then agrees on every
-    rank: it is taken from the all-reduced times)."""
+    the same adjacency and feature shape.
+
+    "auto" (default): the first call runs ONE partition -- a choice "tune"
+    persisted for this node and (world, n, nnz, F, K, library), broadcast
+    from rank 0, else rule_choice (no collective) -- so the call the
+    reference times (reddit.py:43, made once per adjacency) pays no trials.
+    "tune": the same first call; the second call times every candidate (a
+    warm and a timed call each, the slowest rank's time by one all-reduce),
+    keeps the fastest for later calls, persists it (tune_file()) and frees the
+    others' propagators."""
     staging = X.is_cuda and dist.get_backend(group) != "nccl"
     name = partition_name()
-    if name != "auto":
-        return _propagator(csr, group, name, staging).propagate(X, K, output="replicated")
+    if name not in ("auto", "tune"):
+        return _run(_propagator(csr, group, name, staging), X, K)
     world = dist.get_world_size(group)
-    key = ("auto", id(group), world, int(X.shape[1]), int(K))
+    n, F = int(X.shape[0]), int(X.shape[1])
+    key = ("auto", id(group), world, F, int(K))
     rec = csr._plans.get(key)
-    if rec is not None:
-        return _propagator(csr, group, rec["chosen"], staging).propagate(X, K,
-                                                                          output="replicated")
-    # first call: warm every candidate, time one call of each (max over
-    # ranks), keep the fastest; its result is this call's
+    if rec is None:
+        chosen, how = None, "rule"
+        per = persisted_choice(world, n, csr.nnz, F, K, X.device)
+        if per is not None or name == "tune":
+            # agree on rank 0's file (ranks of several nodes may see others)
+            idx = torch.tensor([AUTO_CANDIDATES.index(per) if per else -1], dtype=torch.int64,
+                               device=X.device if dist.get_backend(group) == "nccl" else "cpu")
+            dist.broadcast(idx, dist.get_global_rank(group, 0), group=group)
+            if int(idx.item()) >= 0:
+                chosen, how = AUTO_CANDIDATES[int(idx.item())], "persisted"
+        if chosen is None:
+            chosen = rule_choice(world, n, csr.nnz, F, K)
+        rec = csr._plans[key] = {"chosen": chosen, "how": how, "seconds": None, "calls": 0}
+    rec["calls"] += 1
+    if name == "tune" and rec["how"] == "rule" and rec["calls"] == 2:
+        return _tune(csr, X, K, group, staging, rec)
+    return _run(_propagator(csr, group, rec["chosen"], staging), X, K)
+
+
+def _tune(csr, X, K, group, staging, rec):
+    """Time every candidate (warm + timed call each; the slowest rank's time),
+    keep and persist the fastest, free the rest; returns its X_K."""
+    world = dist.get_world_size(group)
     cands = list(AUTO_CANDIDATES)
-    secs, outs = [], {}
+    secs = []
     for c in cands:
         prop = _propagator(csr, group, c, staging)
-        prop.propagate(X, K, output="replicated")
+        _run(prop, X, K)
         _align(X, group)  # every rank starts the timed call together
         t0 = time.perf_counter()
-        outs[c] = prop.propagate(X, K, output="replicated")
+        out = _run(prop, X, K)
         _sync(X)
         secs.append(time.perf_counter() - t0)
+        del out  # never three X_K alive at once
     slow = _slowest(secs, X, group)
     best = min(range(len(cands)), key=lambda i: (slow[i], i))
-    csr._plans[key] = {"chosen": cands[best], "seconds": dict(zip(cands, slow))}
-    return outs[cands[best]]
+    rec.update(chosen=cands[best], how="timed", seconds=dict(zip(cands, slow)))
+    for c in cands:
+        if c != rec["chosen"]:
+            _drop_propagator(csr, group, c, staging)
+    if dist.get_rank(group) == 0:
+        _persist_choice(world, int(X.shape[0]), csr.nnz, int(X.shape[1]), K, X.device,
+                        rec["chosen"], rec["seconds"])
+    # the winner's result (every candidate's X_K is the same bits)
+    return _run(_propagator(csr, group, rec["chosen"], staging), X, K)
 
 
 # ---------------------------------------------------------------------------
@@ -351,4 +486,5 @@ def feature_blocks(F, parts, align=4):
 
 __all__ = ["torchrun_env", "bind_local_device", "process_group", "precompute_group",
            "devices_from_env", "DeviceSet", "precompute_devices", "feature_blocks",
-           "PARTITIONS", "AUTO_CANDIDATES", "ReplicatedPropagator", "auto_choice"]
+           "PARTITIONS", "AUTO_CANDIDATES", "ReplicatedPropagator", "auto_choice",
+           "rule_choice", "persisted_choice", "tune_file"]

@@ -77,6 +77,24 @@ def main():
     finally:
         D.CHUNK_STREAMS, D.HUB_EARLY = saved
     rec["schedules_equal"] = ok
+    # the replicated last hop through the IPC window (sgc_ipc_get_handle,
+    # sgc_signal_flag_i32 / sgc_wait_flags_i32, sgc_pull_blocks_f32) at one
+    # rank: X, 2X, 4X, X -- the window's halves alternate, so a stale block
+    # would show; power-of-two scaling is exact through every fma
+    ipc_ok = {}
+    scaled = True
+    for name, prop in (("features", FeaturePartitionedPropagator(csr, chunks=4)),
+                       ("lines", LinePartitionedPropagator(make_shard(rp, ci, va, 0, 1, dev),
+                                                           csr=csr, chunks=4))):
+        prop.force_ipc = True
+        outs = [prop.propagate(X * s, 2, output="replicated") for s in (1.0, 2.0, 4.0, 1.0)]
+        torch.cuda.synchronize()
+        ipc_ok[name] = bool(prop._ipc is not None and torch.equal(outs[0], want) and
+                            torch.equal(outs[3], want))
+        scaled = scaled and torch.equal(outs[1], want * 2.0) and torch.equal(outs[2], want * 4.0)
+    rec["ipc_features_equal"] = ipc_ok["features"]
+    rec["ipc_lines_equal"] = ipc_ok["lines"]
+    rec["ipc_scaled_calls_exact"] = bool(scaled)
     # the tail-stream pattern (LinePartitionedPropagator.propagate): gathers
     # issued from a side stream, waited there, then on the main stream
     full = [torch.zeros((64, 96), device=dev) for _ in range(2)]

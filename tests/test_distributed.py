@@ -209,6 +209,30 @@ def test_gathered_layout():
     assert sh.identity_layout and sh.col_gathered is sh.col_idx
 
 
+@pytest.mark.parametrize("name", ["hub1000_F130", "norm_n48_F65", "isolated_F17",
+                                  "raw_unsorted_dups_F7"])
+def test_make_shard_device_matches_host(tiny_cases, name):
+    """The shards the multi-GPU call builds from the adjacency's own arrays
+    (make_shard_device: no host copy of S) equal the host slicing's, bounds,
+    row_ptr, both column-id arrays and values, for every rank at P = 1..8."""
+    from sgc_amd.distributed import make_shard_device
+    from sgc_amd.propagate import csr_of
+    c = tiny_cases[name]
+    n = int(c["n"])
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([c["rows"], c["cols"]])),
+                                  torch.from_numpy(c["vals"]), (n, n))
+    csr = csr_of(adj)
+    rp, ci, va = (t.numpy() for t in (csr.row_ptr, csr.col_idx, csr.val))
+    for world in range(1, 9):
+        for rank in range(world):
+            h = make_shard(rp, ci, va, rank, world, "cpu")
+            d = make_shard_device(csr, rank, world)
+            assert np.array_equal(h.bounds, d.bounds), (world, rank)
+            for f in ("row_ptr", "col_idx", "val", "col_gathered"):
+                assert torch.equal(getattr(h, f), getattr(d, f)), (world, rank, f)
+            assert d.n == h.n and d.block == h.block
+
+
 # ---------------------------------------------------------------------------
 # Cyclic row tiles + column-ordered exchange (CyclicRowPropagator).
 

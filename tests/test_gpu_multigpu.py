@@ -244,6 +244,38 @@ def test_sgc_precompute_under_torchrun_matches_one_gpu(tmp_path, partition):
     for rec in recs:
         assert rec["world"] == 2 and rec["backend"] == "gloo" and rec["repeat_equal"]
         assert rec["sha"] == want
+        assert rec["propagations"] == [1, 1, 1], rec  # no trials in the first call
+        if partition in ("features", "lines"):  # replicated X_K by IPC pulls
+            assert rec["exchange"] == ["ipc"], rec
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_auto_first_call_one_partition_ranks_sharing_gpu(tmp_path, world):
+    """VERDICT r05 item 2 on the GPU: `world` torchrun ranks sharing this GPU
+    run the unchanged sgc_precompute with the default "auto" partition (the
+    minimum-work gate off, so the rule splits at world >= 3): every call,
+    the first included, runs exactly one propagation, and every rank's X_K
+    is one GPU's; the replicated output of a split goes through the IPC
+    window (peers' blocks pulled into X_K, ranks in different processes)."""
+    from drivers.reddit import synthetic_reddit
+    from sgc_amd.multigpu import rule_choice
+    from sgc_amd.utils import sgc_precompute
+    n = 20000
+    r = _torchrun(world, ["tests/rank_precompute.py", str(tmp_path), str(n)],
+                  {"SGC_AMD_AUTO_MIN_WORK": "0"}, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(world)]
+    adj, _, features, _, _, _, _ = synthetic_reddit(n)
+    one, _ = sgc_precompute(features, adj, 2)
+    want = hashlib.sha256(one.cpu().numpy().tobytes()).hexdigest()
+    chosen = rule_choice(world, n, adj._sgc_amd_csr[1].nnz, features.shape[1], 2) \
+        if world > 2 else "replicate"
+    for rec in recs:
+        assert rec["world"] == world and rec["sha"] == want and rec["repeat_equal"], rec
+        assert rec["propagations"] == [1, 1, 1], rec
+        assert rec["auto"]["chosen"] == chosen and rec["auto"]["how"] == "rule", rec
+        if chosen != "replicate":
+            assert rec["exchange"] == ["ipc"], rec
 
 
 def test_rccl_exchange_paths_world1():
@@ -261,6 +293,9 @@ def test_rccl_exchange_paths_world1():
     assert rec["features_replicated_equal"] and rec["lines_replicated_equal"], rec
     assert rec["lines_sharded_equal"] and rec["tail_stream_pattern_ok"], rec
     assert rec["schedules_equal"], rec  # 1:3:3:1 chunks, one / two streams, hub rows early
+    # the IPC window at world 1 (force_ipc): handle, flags, waits, pulls
+    assert rec["ipc_features_equal"] and rec["ipc_lines_equal"], rec
+    assert rec["ipc_scaled_calls_exact"], rec
 
 
 def test_reddit_driver_runs_under_torchrun():
@@ -309,7 +344,7 @@ def dist_cache(tmp_path_factory):
     ("reddit", "rows", []),
     ("reddit", "rows", ["--row-chunks", "4"]),
     ("reddit", "cyclic", ["--groups", "3"]),
-    ("reddit", "features", []),
+    ("reddit", "features", ["--also-replicated"]),
     ("reddit", "lines", ["--also-replicated"]),
     ("reddit", "tiles", ["--col-blocks", "2"]),
     ("rmat", "rows", []),
@@ -320,6 +355,9 @@ def test_p8_partition_full_size_bit_exact(dist_cache, shape, partition, extra):
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _last_json(r.stdout)
     assert rec["world"] == 8 and rec["bit_exact_vs_reference_hash"], rec
+    if "--also-replicated" in extra:  # every rank's full X_K: IPC pulls and the collective
+        assert rec["replicated_exchange"] == ["ipc"], rec
+        assert all(rec["replicated"].values()), rec
 
 
 @pytest.mark.slow

@@ -5,6 +5,7 @@ MFMA classifier (rtol=atol=1e-5 relative to max|ref|, north_star's bar for fp32)
 All calls go through libsgc_amd.so; nothing here may fall back to torch ops
 for the arithmetic under test.
 """
+import functools
 import hashlib
 
 import numpy as np
@@ -232,6 +233,68 @@ def test_shape_hashes(shape, shapes_golden, shape_rows):
         assert sha(Y) == rec["sha"], (shape, K)
 
 
+@functools.lru_cache(maxsize=1)
+def _big_graph(shape, seed):
+    """The seeded BASELINE-shape graph, generated once for the tests that
+    follow each other on it (the RMAT shape takes a minute on the host)."""
+    from sgc_amd import graphs
+    return graphs.synthetic_graph(shape, seed=seed)
+
+
+def device_sha(Y):
+    """SHA-256 of a device tensor's bytes, copied to the host in 256 MB
+    pieces (the same digest as sha(Y.cpu().numpy()))."""
+    h = hashlib.sha256()
+    rows = max(1, (256 << 20) // max(1, 4 * Y.shape[1]))
+    for r in range(0, Y.shape[0], rows):
+        h.update(np.ascontiguousarray(Y[r:r + rows].cpu().numpy()).tobytes())
+    return h.hexdigest()
+
+
+def _public_call_hashes(shape, K, g, calls):
+    """The call bench.py times, as bench.py makes it: the public
+    sgc_precompute(X, adj, K) on a torch COO adjacency moved to the GPU
+    (device ingest + plan + recording on the first call, the recorded launch
+    list replayed on later ones).  `calls` lists, per call, whether it gets
+    the same X tensor ("same") or a fresh copy of it ("new"); every call's
+    result is a new X_K tensor.  Returns each call's output hash."""
+    from sgc_amd import graphs
+    from sgc_amd.utils import sgc_precompute
+    S = _big_graph(shape, g["seed"])
+    X = graphs.synthetic_features(shape, g["n"], g["features"], seed=g["feature_seed"])
+    rows, cols, vals = S.coo()
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([rows, cols])),
+                                  torch.from_numpy(vals), (S.n, S.n)).to(DEV)
+    del rows, cols, vals
+    X0 = torch.from_numpy(X).to(DEV)
+    del X
+    hashes, outs = [], []
+    for kind in calls:
+        Xc = X0 if kind == "same" else X0.clone()
+        out, secs = sgc_precompute(Xc, adj, K)
+        assert secs > 0 and out.shape == X0.shape
+        hashes.append(device_sha(out))
+        outs.append(out.data_ptr())
+        del out, Xc
+    assert getattr(adj, "_sgc_amd_csr", None) is not None  # the CSR was cached
+    del X0, adj
+    torch.cuda.empty_cache()
+    return hashes
+
+
+@pytest.mark.slow
+def test_public_call_reddit_shape_hash_replay(shapes_golden):
+    """the exact call bench.py times at the benched size
+    -- sgc_precompute(features, adj, 2) on the Reddit-shape torch COO (reference
+    reddit.py:43 -> utils.py:92-97) -- hashed on the first call (device ingest,
+    plan, launch-list recording), on a replay with the same X_0 and on a
+    replay with a new X_0 tensor, all against the reference's own hash."""
+    g = shapes_golden["reddit"]
+    want = g["outputs"]["2"]["sha"]
+    hashes = _public_call_hashes("reddit", 2, g, ["same", "same", "new"])
+    assert hashes == [want] * 3, hashes
+
+
 @pytest.mark.slow
 def test_reddit_shape_hash(shapes_golden, shape_rows):
     """Full BASELINE size (233k nodes, 23.4M nnz, F=602, K=2): bit-exact hash
@@ -241,7 +304,7 @@ def test_reddit_shape_hash(shapes_golden, shape_rows):
     from sgc_amd import graphs
     from sgc_amd.propagate import DeviceCSR, propagate
     g = shapes_golden["reddit"]
-    S = graphs.synthetic_graph("reddit", seed=g["seed"])
+    S = _big_graph("reddit", g["seed"])
     rows, cols, vals = S.coo()
     assert sha(np.stack([rows, cols])) == g["sha_indices"]
     assert sha(vals) == g["sha_values"]
@@ -265,7 +328,7 @@ def test_rmat_shape_hash(shapes_golden, shape_rows):
     from sgc_amd import graphs
     from sgc_amd.propagate import DeviceCSR, propagate
     g = shapes_golden["rmat"]
-    S = graphs.synthetic_graph("rmat", seed=g["seed"])
+    S = _big_graph("rmat", g["seed"])
     rows, cols, vals = S.coo()
     assert sha(np.stack([rows, cols])) == g["sha_indices"]
     assert sha(vals) == g["sha_values"]
@@ -278,6 +341,16 @@ def test_rmat_shape_hash(shapes_golden, shape_rows):
     Y = propagate(csr, Xd.to(DEV), 3).cpu().numpy()
     assert bits_equal(Y[shape_rows["rmat_rows"]], shape_rows["rmat_K3"])
     assert sha(Y) == g["outputs"]["3"]["sha"]
+
+
+@pytest.mark.slow
+def test_public_call_rmat_shape_hash_replay(shapes_golden):
+    """BASELINE config 5 through the public call as bench.py times it: the
+    first call (device ingest of 260 M COO entries, plan, recording) and one
+    launch-list replay with a new X_0, hashed against the reference's X_3."""
+    g = shapes_golden["rmat"]
+    hashes = _public_call_hashes("rmat", 3, g, ["same", "new"])
+    assert hashes == [g["outputs"]["3"]["sha"]] * 2, hashes
 
 
 @pytest.mark.parametrize("F", [64, 130, 192])
