@@ -409,6 +409,9 @@ int sgc_linear_f32(const float *X, int64_t ldx, const float *W, const float *b,
  * current "linear_kernel" tuning), for benchmark labels; "none" for an empty
  * or invalid shape.  Static storage. */
 const char *sgc_linear_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C, const float *X);
+/* The weight-backward kernel sgc_linear_backward_f32 runs for this shape /
+ * alignment (static string; bench labels). */
+const char *sgc_linear_backward_kernel_name(int64_t M, int64_t K, int64_t ldx, const float *X);
 
 /* Backward of sgc_linear_f32 for the weights (what autograd runs for
  * nn.Linear after F.cross_entropy(model(x), y).backward() in the closures of

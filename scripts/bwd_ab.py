@@ -22,7 +22,11 @@ def main():
     ap.add_argument("--rows", type=int, default=152410)
     ap.add_argument("--features", type=int, default=602)
     ap.add_argument("--classes", type=int, default=41)
+    ap.add_argument("--kernel", type=int, default=0,
+                    help="sgc_set_tuning('backward_kernel'): 0 auto, 1 fp32 slabs, 2 split-bf16")
     a = ap.parse_args()
+    from sgc_amd import _lib
+    _lib.check(_lib.load().sgc_set_tuning(b"backward_kernel", a.kernel), "set_tuning")
     g = torch.Generator().manual_seed(0)
     x = torch.randn(a.rows, a.features, generator=g)
     dy = torch.randn(a.rows, a.classes, generator=g) / a.rows
@@ -31,8 +35,12 @@ def main():
     dW, db = linear_backward(xd, dyd)
     ref = dy.double().t() @ x.double()
     err = ((dW.cpu().double() - ref).abs().max() / ref.abs().max()).item()
-    print(json.dumps({"lib": os.environ.get("SGC_AMD_LIB", "default"), "backward_ms": ms,
-                      "rel_err": err}), flush=True)
+    refb = dy.double().sum(0)
+    errb = ((db.cpu().double() - refb).abs().max() / refb.abs().max()).item()
+    name = _lib.load().sgc_linear_backward_kernel_name(a.rows, a.features, xd.stride(0),
+                                                       _lib.ptr(xd)).decode()
+    print(json.dumps({"lib": os.environ.get("SGC_AMD_LIB", "default"), "kernel": name,
+                      "backward_ms": ms, "rel_err": err, "db_rel_err": errb}), flush=True)
 
 
 if __name__ == "__main__":

@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--stages", action="store_true", help="time the tiny call's stages first")
     ap.add_argument("--warm", action="store_true",
                     help="call propagate.warmup() first (what the drop-in loaders do)")
+    ap.add_argument("--reserve-gb", type=float, default=0.0,
+                    help="allocate and free this many GiB first (held in torch's cache)")
     ap.add_argument("--no-tiny", action="store_true",
                     help="skip the tiny call: first_call_s is the process's first call")
     args = ap.parse_args()
@@ -49,7 +51,14 @@ def main():
     Xt = torch.from_numpy(graphs.synthetic_features("cora", T.n, F, seed=1)).to(dev)
     at, a1, a2 = coo(T, dev), coo(S, dev), coo(S, dev)
     torch.cuda.synchronize()
-    rec = {"shape": args.shape, "warm": args.warm, "tiny": not args.no_tiny}
+    rec = {"shape": args.shape, "warm": args.warm, "tiny": not args.no_tiny,
+           "reserve_gb": args.reserve_gb}
+    if args.reserve_gb > 0:
+        t = time.perf_counter()
+        blk = torch.empty(int(args.reserve_gb * 2**30), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        del blk
+        rec["reserve_s"] = round(time.perf_counter() - t, 4)
     if args.warm:
         from sgc_amd.propagate import warmup
         rec["warmup_s"] = round(warmup(dev), 4)

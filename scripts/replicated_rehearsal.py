@@ -47,7 +47,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from sgc_amd import graphs  # noqa: E402
-from sgc_amd.distributed import (FeaturePartitionedPropagator,  # noqa: E402
+from sgc_amd.distributed import (IPC_DONE, IPC_FLAG_WORDS,  # noqa: E402
+                                 FeaturePartitionedPropagator, IpcPeers,
                                  LinePartitionedPropagator, _copy_blocks, feature_bounds,
                                  line_bounds, make_shard, replicated_chunks)
 from sgc_amd.propagate import DeviceCSR, propagate  # noqa: E402
@@ -62,6 +63,8 @@ class _Local:
 
     def _reset_marks(self):
         self.marks = []
+        if getattr(self, "_ipc", None) is not None:
+            self._ipc._marks = self.marks
 
     def _mark(self, dst):
         ev = torch.cuda.Event(enable_timing=True)
@@ -89,6 +92,53 @@ class LocalFeatures(_Local, FeaturePartitionedPropagator):
         if m:
             recv[:m].copy_(send[:m])
         return []
+
+
+class LocalIpcPeers(IpcPeers):
+    """The IPC window of a rehearsed rank: every "peer" maps to this rank's
+    own window (pulls read P blocks at local HBM speed: on a node the P - 1
+    peer blocks come over the links, their reads land on the peers' HBM and
+    the pulls' writes on this rank's); chunk flags record a timing event (the
+    chunk's readiness) when raised."""
+
+    def __init__(self, rank, world, n, ld, device, marks):
+        self.rank, self.world, self.n, self.ld = rank, world, int(n), int(ld)
+        half = self.n * self.ld
+        self.window = torch.zeros(2 * half + IPC_FLAG_WORDS, dtype=torch.float32, device=device)
+        self.flags = self.window[2 * half:].view(torch.int32)
+        self.halves = [self.window[:half].view(self.n, self.ld),
+                       self.window[half:2 * half].view(self.n, self.ld)]
+        self.err = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self.ptrs = [self.window.data_ptr()] * world
+        self._bases = []
+        self.seq = 0
+        self._marks = marks
+
+    def signal(self, word, value, stream):
+        super().signal(word, value, stream)
+        if word < IPC_DONE:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+            self._marks.append((ev, 0))
+
+
+def _ipc_rehearsal(enable):
+    """Route the feature / line partitions' replicated last hop through
+    LocalIpcPeers (enable) or through the collective path (not)."""
+    import sgc_amd.distributed as D
+    if not enable:
+        os.environ["SGC_AMD_REPLICATED_EXCHANGE"] = "collective"
+        return
+    os.environ["SGC_AMD_REPLICATED_EXCHANGE"] = "ipc"
+
+    def fake(prop, group, rank, world, n, ld, device):
+        key = (n, ld, str(device))
+        if getattr(prop, "_ipc_key", None) != key:
+            prop._ipc = LocalIpcPeers(rank, world, n, ld, device, prop.marks)
+            prop._ipc_key = key
+        prop._ipc._marks = prop.marks
+        return prop._ipc
+    D._ipc_for = fake
 
 
 class LocalLines(_Local, LinePartitionedPropagator):
@@ -198,9 +248,14 @@ def main():
     ap.add_argument("--fractions", default="",
                     help="semicolon-separated row fractions of the last hop's chunks to "
                          "compare, e.g. 1,3,3,1;1,1,2,3,1 (sgc_amd.distributed.REPLICATED_CHUNKS)")
+    ap.add_argument("--exchange", default="ipc", choices=["ipc", "collective"],
+                    help="the replicated last hop: IPC pulls of the peers' blocks straight "
+                         "into X_K (the product's default on a GPU node) or in-place "
+                         "all-gathers + unpack")
     ap.add_argument("--chunks", type=int, default=4,
                     help="last-hop chunks (4 = the product's 1:3:3:1 split, else equal)")
     args = ap.parse_args()
+    _ipc_rehearsal(args.exchange == "ipc")
     spec = graphs.SHAPES[args.shape]
     S = graphs.synthetic_graph(args.shape, seed=0)
     F, K, n = spec["features"], spec["hops"], S.n
@@ -255,22 +310,27 @@ def run_schedule(args, S, csr, X0, out, t1, F, K, n, sched):
                 # the chunk timeline alone and under a concurrent copy of the
                 # gather's bytes ((P-1)/P of X_K, read + written)
                 step0, ready0 = timeline(prop, X0, K, args.reps)
-                nb = int((P - 1) / P * n * F)
-                src = torch.empty(nb, device="cuda")
-                dst = torch.empty(nb, device="cuda")
-                step1, ready1 = timeline(prop, X0, K, args.reps, copy=(src, dst))
-                del src, dst
                 import sgc_amd.distributed as D
                 chunks = replicated_chunks(n, D.REPLICATED_CHUNKS if prop.chunks == 4
                                            else (1,) * prop.chunks)
                 gbytes = [(P - 1) * (r1 - r0) * wcols * 4 for r0, r1 in chunks]
-                # one chunk's unpack (the block-copy launch of P blocks)
-                r0, r1 = chunks[-1]
-                rows = r1 - r0
-                full = prop._bufs[("full", len(chunks) - 1)]
-                cb = [(q * rows, 0, r0, min(q * wcols, F), rows,
-                       min((q + 1) * wcols, F) - min(q * wcols, F)) for q in range(P)]
-                t_unpack = timeit(lambda: _copy_blocks(full, out, cb), args.reps)
+                if args.exchange == "ipc":
+                    # the pulls are in the step (P blocks read at local HBM
+                    # speed and written into X_K): no side copy, no unpack
+                    step1, ready1, t_unpack = step0, ready0, 0.0
+                else:
+                    nb = int((P - 1) / P * n * F)
+                    src = torch.empty(nb, device="cuda")
+                    dst = torch.empty(nb, device="cuda")
+                    step1, ready1 = timeline(prop, X0, K, args.reps, copy=(src, dst))
+                    del src, dst
+                    # one chunk's unpack (the block-copy launch of P blocks)
+                    r0, r1 = chunks[-1]
+                    rows = r1 - r0
+                    full = prop._bufs[("full", len(chunks) - 1)]
+                    cb = [(q * rows, 0, r0, min(q * wcols, F), rows,
+                           min((q + 1) * wcols, F) - min(q * wcols, F)) for q in range(P)]
+                    t_unpack = timeit(lambda: _copy_blocks(full, out, cb), args.reps)
                 tail_exposed = 0.0
                 if cand == "lines" and F - line_bounds(F, P)[1] > 0:
                     # each hop's tail gather beside that hop's main launch
@@ -278,8 +338,10 @@ def run_schedule(args, S, csr, X0, out, t1, F, K, n, sched):
                     tb = (P - 1) * shard.block * prop._tail_ld * 4
                     tail_exposed = K * max(0.0, tb / ingress * 1e3 - step0 / (K + 1))
                 proj = project(step1, ready1, gbytes, t_unpack, ingress) + tail_exposed
-                bd = breakdown(prop, X0, K, args.reps) if args.breakdown else None
-                rec = {"case": "rank", "schedule": sched, "P": P, "candidate": cand, "rank": p,
+                bd = breakdown(prop, X0, K, args.reps) if (args.breakdown and
+                                                            args.exchange == "collective") else None
+                rec = {"case": "rank", "schedule": sched, "exchange": args.exchange, "P": P,
+                       "candidate": cand, "rank": p,
                        "block_cols": wcols, "compute_replicated_ms": t_rep,
                        "compute_sharded_ms": t_sh, "replication_local_ms": t_rep - t_sh,
                        "step_ms": step0, "chunk_ready_ms": ready0,
@@ -298,7 +360,8 @@ def run_schedule(args, S, csr, X0, out, t1, F, K, n, sched):
                 best[cand] = max(r["projected_replicated_ms"] for r in recs)
                 rank_recs[cand] = recs
         chosen = min(best, key=best.get)
-        summ = {"case": "summary", "schedule": sched, "P": P, "single_ms": t1, "link_GBps_each_way": args.link_gbps,
+        summ = {"case": "summary", "schedule": sched, "exchange": args.exchange, "P": P,
+                "single_ms": t1, "link_GBps_each_way": args.link_gbps,
                 "projected_ms": best, "projected_speedup": {c: t1 / v for c, v in best.items()},
                 "auto_would_choose": chosen, "auto_speedup": t1 / best[chosen],
                 "replication_local_ms_max": {c: max(r["replication_local_ms"] for r in rs)

@@ -19,6 +19,24 @@ import os
 import sys
 
 
+def kernel_label(name):
+    """'void sgc::(anonymous namespace)::xent_dw_kernel<2, 3, 2>(float const*, ...)'
+    -> 'xent_dw_kernel<2, 3, 2>' (the anonymous namespace's parentheses must
+    go before the argument list is cut: round 5's summaries cut at them and
+    labelled every kernel '')."""
+    k = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    depth, cut = 0, len(k)
+    for i, ch in enumerate(k):  # the first '(' outside the template arguments
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            cut = i
+            break
+    return k[:cut].split("::")[-1].strip() if "::" in k[:cut].split("<")[0] else k[:cut].strip()
+
+
 def main(d):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -28,8 +46,7 @@ def main(d):
     for fn in files:
         with open(fn) as f:
             for r in csv.DictReader(f):
-                k = r.get("Kernel_Name", "").split("(")[0].split("<")[0].replace("void ", "")
-                k = k.split("::")[-1]
+                k = kernel_label(r.get("Kernel_Name", ""))
                 did = r.get("Dispatch_Id", r.get("Correlation_Id", ""))
                 per[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[k].add(did)

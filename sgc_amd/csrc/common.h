@@ -66,6 +66,8 @@ extern int g_tile_buffers;
 extern int g_linear_kernel;
 // k per chunk of the streaming classifier kernel (32 or 64).
 extern int g_linear_ck;
+// Classifier weight backward: 0 auto, 1 fp32 MFMA slabs, 2 split-bf16 slabs (xent.hip).
+extern int g_backward_kernel;
 
 template <int V> struct Vec { typedef float __attribute__((ext_vector_type(V))) T; };
 template <> struct Vec<1> { typedef float T; };

@@ -1686,6 +1686,11 @@ int set_tuning(const char *key, int64_t value) {
         g_linear_kernel = (int)value;
         return SGC_OK;
     }
+    if (std::string(key) == "backward_kernel") {
+        SGC_REQUIRE(value >= 0 && value <= 2, SGC_EINVAL, "backward_kernel must be 0..2");
+        g_backward_kernel = (int)value;
+        return SGC_OK;
+    }
     if (std::string(key) == "max_vec") {
         SGC_REQUIRE(value == 1 || value == 2 || value == 4, SGC_EINVAL, "max_vec must be 1, 2 or 4");
         g_max_vec = (int)value;
@@ -1707,6 +1712,7 @@ int64_t get_tuning(const char *key) {
     if (key && std::string(key) == "tile_buffers") return g_tile_buffers;
     if (key && std::string(key) == "linear_kernel") return g_linear_kernel;
     if (key && std::string(key) == "linear_ck") return g_linear_ck;
+    if (key && std::string(key) == "backward_kernel") return g_backward_kernel;
     return -1;
 }
 

