@@ -294,7 +294,16 @@ __global__ __launch_bounds__(256) void xent_dw_kernel(const float *__restrict__ 
 //             splits its 16 values, and runs 3 x 2 x 6 MFMAs against the LDS
 //             pieces per 32 rows, the next step's X loads in flight.
 // No transpose, one split of dY per slab (round 6's first form split it on
-// every pass: 25 M VALU, slower than fp32).  Products hh go to accH, the five
+// every pass: 25 M VALU, slower than fp32).
+// Measured (Reddit-train shape, rocprofv3 kernel means, profiles/r06/s8*):
+// 107 us against the fp32 slabs' 112-115 us, but 681 slabs of 224 rows make
+// the reduction 19.6 us against 16.3 (512 slabs): 127 vs 131 us in all, within
+// run-to-run spread, so it stays opt-in (sgc_set_tuning("backward_kernel", 2)).
+// Not kept: 16-B lanes over 64-column groups (115 us), 320-row slabs in two
+// LDS phases (126 us), 160 / 128-row slabs (115 / 121 us + 28 / 35 us of
+// reduction), a register cap for two workgroups per CU (spills: 256 us).
+// The counters (profiles/r06/s6) put it at 58 % issue-stalled with MFMA busy
+// 21 us of the 107: neither the MFMA nor the X stream (3.4 TB/s) bounds it.  Products hh go to accH, the five
 // small ones to accL (as the forward kernel); dW = accH + accL per slab.
 // Rows past the slab and classes >= C read 0 through the descriptors.
 constexpr int kDwSplitRows = 224;  // slab rows (7 steps): 7 x 3 x 3 KB of LDS pieces
@@ -518,20 +527,30 @@ __global__ __launch_bounds__(256) void xent_reduce_dw_db_kernel(
             for (; j < j1; ++j) s += p[(int64_t)j * stride];
         }
     } else {
-        e = (blockIdx.x - dw_blocks) * 64LL + lane;  // class
-        ok = e < C;
-        if (ok)
-            for (int j = j0; j < j1; ++j) s += db_slab[(int64_t)j * C16 + e];
+        // db: one wave per class -- lane l sums slabs l, l + 64, ... (eight
+        // loads in flight), then a fixed xor tree across the wave (round 6's
+        // first form had one lane walk a quarter of the slabs: 49 us)
+        const int cls = (blockIdx.x - dw_blocks) * 4 + w;
+        if (cls < C) {
+            const float *p = db_slab + cls;
+            int j = lane;
+            for (; j + 7 * 64 < n_slabs; j += 8 * 64) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(j + u * 64) * C16];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s += v[u];
+            }
+            for (; j < n_slabs; j += 64) s += p[(int64_t)j * C16];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+            if (lane == 0) db[cls] = s;
+        }
+        return;  // (uniform per block: no barrier below is reached)
     }
     part[w][lane] = s;
     __syncthreads();
-    if (w == 0 && ok) {
-        const float r = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
-        if ((int)blockIdx.x < dw_blocks)
-            dW[e] = r;
-        else
-            db[e] = r;
-    }
+    if (w == 0 && ok) dW[e] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
 // loss (double, block C) and db (block c < C): 256 threads per block, strided
@@ -791,7 +810,7 @@ int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ld
                 hipGetErrorString(e));
     // dW and db in one launch (fixed-order sums over the slabs)
     const int dw_blocks = (int)((C * K + 63) / 64);
-    const int db_blocks = db ? (int)((C + 63) / 64) : 0;
+    const int db_blocks = db ? (int)((C + 3) / 4) : 0;  // a wave per class
     hipLaunchKernelGGL(xent_reduce_dw_db_kernel, dim3((unsigned)(dw_blocks + db_blocks)),
                        dim3(256), 0, s, slab, n_slabs, (int)C, (int)K, C16, dW, db_slab, db,
                        dw_blocks);

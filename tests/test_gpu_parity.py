@@ -954,13 +954,27 @@ def test_logits_cross_entropy_matches_torch(M, C, ldl):
 
 
 def test_logits_cross_entropy_bad_label_gives_nan():
-    """A label outside [0, C) (not ignore_index): the loss is NaN (torch
-    stops with a device assert), no fault."""
+    """At the C ABI (sgc_cross_entropy_f32, no host check) a label outside
+    [0, C) that is not ignore_index makes the loss NaN, without a fault; the
+    Python boundary raises before launching (test_logits_cross_entropy_
+    rejects_out_of_range_labels)."""
+    from sgc_amd import _lib
     from sgc_amd.models import SGCLogits
-    x = torch.randn(50, 5, device=DEV).as_subclass(SGCLogits)
+    lib = _lib.load()
+    x = torch.randn(50, 5, device=DEV)
     y = torch.randint(0, 5, (50,), device=DEV)
     y[3] = 9
-    assert torch.isnan(torch.nn.functional.cross_entropy(x, y)).item()
+    loss = torch.empty((), device=DEV)
+    inv = torch.empty(1, device=DEV)
+    lse = torch.empty(50, device=DEV)
+    wsb = lib.sgc_cross_entropy_workspace(50, 5)
+    ws = torch.empty(max(1, wsb), dtype=torch.uint8, device=DEV)
+    _lib.check(lib.sgc_cross_entropy_f32(_lib.ptr(x), 5, _lib.ptr(y), 50, 5, -100, _lib.ptr(loss),
+                                         _lib.ptr(inv), _lib.ptr(lse), _lib.ptr(ws), wsb,
+                                         _lib.stream_handle()), "cross_entropy_f32")
+    assert torch.isnan(loss).item()
+    with pytest.raises(IndexError):
+        torch.nn.functional.cross_entropy(x.as_subclass(SGCLogits), y)
 
 
 def test_unchanged_closure_uses_the_hip_loss():
