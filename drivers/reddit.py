@@ -72,7 +72,10 @@ def synthetic_reddit(n, seed=0):
     norm = fetch_normalization("AugNormAdj")
     adj = sparse_mx_to_torch_sparse_tensor(norm(A)).float()
     train_adj = sparse_mx_to_torch_sparse_tensor(norm(A[tr][:, tr])).float()
-    return adj.cuda(), train_adj.cuda(), feats.cuda(), labels.cuda(), tr, va, te
+    out = (adj.cuda(), train_adj.cuda(), feats.cuda(), labels.cuda(), tr, va, te)
+    from sgc_amd.propagate import warmup
+    warmup(out[2].device)  # as load_reddit_data does once the data is on the GPU
+    return out
 
 
 def train_regression(model, train_features, train_labels, epochs):
