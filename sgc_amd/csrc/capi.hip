@@ -555,6 +555,7 @@ int sgc_warmup(uint32_t units, void *stream) {
     SGC_REQUIRE((units & ~7u) == 0, SGC_EINVAL, "warmup: unknown unit bits 0x%x", units);
     hipStream_t s = as_stream(stream);
     if (units & SGC_WARM_PROPAGATE) {
+        SGC_HIP_CHECK(warm_side_streams());  // the SpMM's side-stream pool
         SGC_HIP_CHECK(warm_spmm(s));
         SGC_HIP_CHECK(warm_ingest(s));
         SGC_HIP_CHECK(warm_plan(s));

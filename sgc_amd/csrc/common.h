@@ -44,6 +44,7 @@ static constexpr int kWave = 64;  // CDNA wavefront width (never 32)
         return hipGetLastError();                                           \
     }
 hipError_t warm_spmm(hipStream_t);
+hipError_t warm_side_streams();  // creates the SpMM's per-device side-stream pool
 hipError_t warm_ingest(hipStream_t);
 hipError_t warm_plan(hipStream_t);
 hipError_t warm_sort(hipStream_t);

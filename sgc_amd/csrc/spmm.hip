@@ -1400,20 +1400,56 @@ struct SideStream {
     std::mutex mu;
 };
 
-hipError_t side_stream(SideStream **out, hipStream_t caller) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, SideStream> per_dev;
+// The side streams themselves come from a small per-device pool, created
+// once (sgc_warmup creates it, with the loaders): hipStreamCreate took 7.8 ms
+// for the process's first side stream (a new hardware queue), inside the first
+// sgc_precompute the reference times (profiles/r06/s10: the first Reddit-shape
+// call 16.2 ms against 8.2 on a second adjacency).  Caller streams take pool
+// streams in turn; past kSidePool callers two callers share one (their light
+// kernels then serialise on it: still correct, ordered by their own events).
+constexpr int kSidePool = 4;
+static std::mutex g_side_mu;
+
+static hipError_t side_pool(int dev, hipStream_t **pool) {
+    static std::map<int, std::vector<hipStream_t>> pools;
+    std::vector<hipStream_t> &v = pools[dev];
+    if (v.empty()) {
+        // (a highest-priority side stream measured neutral, +-1%:
+        // profiles/r01_hub_priority_sweep.log)
+        for (int k = 0; k < kSidePool; ++k) {
+            hipStream_t st = nullptr;
+            hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+            if (e != hipSuccess) return e;
+            v.push_back(st);
+        }
+    }
+    *pool = v.data();
+    return hipSuccess;
+}
+
+hipError_t warm_side_streams_impl() {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    std::lock_guard<std::mutex> lock(mu);
+    std::lock_guard<std::mutex> lock(g_side_mu);
+    hipStream_t *pool = nullptr;
+    return side_pool(dev, &pool);
+}
+
+hipError_t side_stream(SideStream **out, hipStream_t caller) {
+    static std::map<std::pair<int, hipStream_t>, SideStream> per_dev;
+    static std::map<int, int> next_pool;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(g_side_mu);
     SideStream &ss = per_dev[{dev, caller}];
     if (!ss.s) {
-        // (a highest-priority side stream measured neutral, +-1%:
-        // profiles/r01_hub_priority_sweep.log)
-        if ((e = hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking)) != hipSuccess) return e;
+        hipStream_t *pool = nullptr;
+        if ((e = side_pool(dev, &pool)) != hipSuccess) return e;
         if ((e = hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming)) != hipSuccess) return e;
         if ((e = hipEventCreateWithFlags(&ss.join, hipEventDisableTiming)) != hipSuccess) return e;
+        ss.s = pool[next_pool[dev]++ % kSidePool];
     }
     *out = &ss;
     return hipSuccess;
@@ -2196,5 +2232,7 @@ int light_order(const int32_t *row_ptr, int64_t row_begin, int64_t row_end, int3
 }
 
 SGC_WARM_UNIT(warm_spmm)
+
+hipError_t warm_side_streams() { return warm_side_streams_impl(); }
 
 }  // namespace sgc

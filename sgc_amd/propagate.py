@@ -845,6 +845,10 @@ def warmup(device=None, units=WARM_PROPAGATE | WARM_CLASSIFIER):
             propagate(csr_of(adj), torch.ones((n, 8), device=dev), 2)
         torch.cuda.synchronize(dev)
         if units & WARM_PROPAGATE:
+            # torch's stream pool for this device (the multi-GPU partitions'
+            # chunk / tail streams): its first use creates the pool's streams,
+            # new hardware queues among them (~8 ms each, profiles/r06/s10)
+            torch.cuda.Stream(device=dev)
             # under torchrun: the process group the partitioned sgc_precompute
             # uses is set up here, with the loaders (rendezvous and RCCL's
             # communicator, eagerly bound to this device), not inside the
