@@ -75,7 +75,10 @@ const char *sgc_last_error(void);
  *                   W^T fits LDS and M >= 4096), 1 = LDS tile, 2 = streaming
  *                   (3 / 4: its diagnostic forms -- loads only / MFMAs only --
  *                   whose results are wrong by design);
- *   "linear_ck":    k per chunk of the streaming forward, 64 (default) or 32.
+ *   "linear_ck":    k per chunk of the streaming forward, 64 (default) or 32;
+ *   "backward_kernel": classifier weight backward, 0 = auto (the fp32 MFMA
+ *                   slabs), 1 = fp32 MFMA slabs, 2 = split-bf16 slabs where X
+ *                   gives 8-B lanes (K and ldx even).
  * sgc_get_tuning returns -1 for an unknown key. */
 int sgc_set_tuning(const char *key, int64_t value);
 int64_t sgc_get_tuning(const char *key);
