@@ -2,7 +2,7 @@
 # round 6 session 1: the new parity tests (public call at full size, IPC
 # exchange at world 1 and with ranks sharing the GPU, first-call partitions)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}" || exit 2
-O=gpurun_out/r06_s1
+O=gpurun_out/r06_s1${TAG:-}
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 T="python -u -m pytest -x -v --timeout-method thread -m gpu"

@@ -1301,6 +1301,7 @@ def _replicated_last_hop(prop, n, P, p, ld, X0, hop_into, gather, unpack):
 IPC_TIMEOUT_US = 20_000_000  # a peer silent this long: the call raises
 IPC_FLAG_WORDS = 64          # int32 flags after the two halves: chunk c ready = word c,
 IPC_DONE = 32                # this rank's pulls of a call done = word 32
+IPC_TEST = 40                # the set-up self-test's flag
 
 
 def replicated_exchange_mode(X0, world, force=False):
@@ -1338,19 +1339,32 @@ class IpcPeers:
         from . import _lib
         lib = _lib.load()
         self.rank, self.world, self.n, self.ld = rank, world, int(n), int(ld)
-        half = self.n * self.ld
-        self.window = torch.empty(2 * half + IPC_FLAG_WORDS, dtype=torch.float32, device=device)
-        self.flags = self.window[2 * half:].view(torch.int32)
-        self.flags.zero_()
-        self.halves = [self.window[:half].view(self.n, self.ld),
-                       self.window[half:2 * half].view(self.n, self.ld)]
-        self.err = torch.zeros(1, dtype=torch.int32).pin_memory()
-        torch.cuda.synchronize(device)  # zeroed flags before any peer reads them
-        h = ctypes.create_string_buffer(128)
-        _lib.check(lib.sgc_ipc_get_handle(_lib.ptr(self.window), h), "ipc_get_handle")
-        handles = [None] * world
-        dist.all_gather_object(handles, h.raw, group=group)
         self.ptrs, self._bases = [], []
+        half = self.n * self.ld
+        mine, why = None, ""
+        try:
+            self.window = torch.empty(2 * half + IPC_FLAG_WORDS, dtype=torch.float32,
+                                      device=device)
+            self.flags = self.window[2 * half:].view(torch.int32)
+            self.flags.zero_()
+            self.halves = [self.window[:half].view(self.n, self.ld),
+                           self.window[half:2 * half].view(self.n, self.ld)]
+            self.err = torch.zeros(1, dtype=torch.int32).pin_memory()
+            torch.cuda.synchronize(device)  # zeroed flags before any peer reads them
+            h = ctypes.create_string_buffer(128)
+            if lib.sgc_ipc_get_handle(_lib.ptr(self.window), h) == 0:
+                mine = h.raw
+            else:
+                why = lib.sgc_last_error().decode(errors="replace")
+        except Exception as e:  # noqa: BLE001 -- reported after the exchange
+            why = f"{type(e).__name__}: {e}"
+        # every rank takes part in the exchange, whatever its own outcome (a
+        # rank raising before it would leave the others in the collective)
+        handles = [None] * world
+        dist.all_gather_object(handles, mine, group=group)
+        if any(x is None for x in handles):
+            raise RuntimeError("sgc_amd: a rank could not export its IPC window" +
+                               (f": {why}" if why else ""))
         try:
             for q in range(world):
                 if q == rank:
@@ -1392,7 +1406,7 @@ class IpcPeers:
             ctypes_void(self.flag_ptr(self.rank, word)), int(value),
             ctypes_void(stream.cuda_stream)), "signal_flag_i32")
 
-    def wait(self, word, value, stream, ranks=None):
+    def wait(self, word, value, stream, ranks=None, timeout_us=IPC_TIMEOUT_US):
         import ctypes
         from . import _lib
         ranks = range(self.world) if ranks is None else list(ranks)
@@ -1402,9 +1416,39 @@ class IpcPeers:
         arr = (ctypes.c_int64 * len(ptrs))(*ptrs)
         _lib.check(_lib.load().sgc_wait_flags_i32(len(ptrs), arr, int(value),
                                                   ctypes_void(self.err.data_ptr()),
-                                                  IPC_TIMEOUT_US,
+                                                  int(timeout_us),
                                                   ctypes_void(stream.cuda_stream)),
                    "wait_flags_i32")
+
+    def self_test(self, timeout_us=5_000_000):
+        """Once, after mapping: every rank writes rank + 1 into the first row
+        of its half 0 and raises flag IPC_TEST; every rank waits for its
+        peers' flags and pulls their first rows.  True when each pulled value
+        is its peer's rank + 1 -- the mapping, the flags' visibility and the
+        pulls work between these processes (and GPUs); else the group keeps
+        the collective path (a wrong byte would otherwise reach X_K)."""
+        import ctypes
+        from . import _lib
+        stream = torch.cuda.current_stream(self.window.device)
+        w = max(1, min(self.ld, 64))
+        self.halves[0][0, :w].fill_(float(self.rank + 1))
+        self.signal(IPC_TEST, 1, stream)
+        self.wait(IPC_TEST, 1, stream, ranks=[q for q in range(self.world) if q != self.rank],
+                  timeout_us=timeout_us)
+        got = torch.zeros((1, w * self.world), dtype=torch.float32, device=self.window.device)
+        segs = [(self.half_ptr(q, 0, 0), self.ld, 0, q * w, 1, w) for q in range(self.world)]
+        for i in range(0, len(segs), 16):
+            part = segs[i:i + 16]
+            arr = (ctypes.c_int64 * (6 * len(part)))(*[v for sg in part for v in sg])
+            _lib.check(_lib.load().sgc_pull_blocks_f32(len(part), arr, _lib.ptr(got), got.stride(0),
+                                                       ctypes_void(stream.cuda_stream)),
+                       "pull_blocks_f32")
+        stream.synchronize()
+        if int(self.err[0]) != 0:
+            self.err.zero_()
+            return False
+        want = torch.arange(1, self.world + 1, dtype=torch.float32).repeat_interleave(w)
+        return bool(torch.equal(got.cpu()[0], want))
 
     def check(self, stream):
         """After the caller's stream is done: raise if a wait timed out."""
@@ -1430,6 +1474,8 @@ def _ipc_for(prop, group, rank, world, n, ld, device):
     ok, ipc, why = 1, None, ""
     try:
         ipc = IpcPeers(group, rank, world, n, ld, device)
+        if not ipc.self_test():
+            ok, why = 0, "the set-up self-test read a wrong value or timed out"
     except Exception as e:  # noqa: BLE001 -- recorded, agreed on below
         ok, why = 0, f"{type(e).__name__}: {e}"
     if world > 1:

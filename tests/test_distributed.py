@@ -567,3 +567,59 @@ def test_sharded_trainer_matches_single_process_lbfgs(world):
         np.testing.assert_allclose(w, model.W.weight.detach().numpy(), rtol=5e-3, atol=1e-4)
         np.testing.assert_allclose(b, model.W.bias.detach().numpy(), rtol=5e-3, atol=1e-4)
         assert np.array_equal(w, results[0][0])  # identical on every rank
+
+
+def _ipc_agreement_worker(rank, world, port, fail_rank, test_fail_rank, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sgc_amd.distributed as D
+
+        class FakePeers:
+            closed = False
+
+            def __init__(self, group, rank_, world_, n, ld, device):
+                if rank_ == fail_rank:
+                    raise RuntimeError("no IPC here")
+
+            def self_test(self):
+                return rank != test_fail_rank
+
+            def close(self):
+                FakePeers.closed = True
+
+        D.IpcPeers = FakePeers
+
+        class Prop:
+            pass
+        prop = Prop()
+        ipc = D._ipc_for(prop, dist.group.WORLD, rank, world, 10, 32, torch.device("cpu"))
+        again = D._ipc_for(prop, dist.group.WORLD, rank, world, 10, 32, torch.device("cpu"))
+        q.put((rank, ipc is not None, again is ipc, getattr(prop, "ipc_unavailable", None)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank,test_fail_rank", [(-1, -1), (0, -1), (-1, 1), (2, 0)])
+def test_ipc_window_is_all_or_none(fail_rank, test_fail_rank):
+    """The IPC exchange is used by every rank or by none: a rank that cannot
+    map its peers (or whose set-up self-test reads a wrong value) makes the
+    whole group keep the collective path -- a MIN all-reduce of the outcome --
+    and the decision is cached on the propagator (one set-up per shape)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ipc_agreement_worker,
+                         args=(r, world, port, fail_rank, test_fail_rank, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = fail_rank < 0 and test_fail_rank < 0
+    for r in range(world):
+        used, cached, why = got[r]
+        assert used == want and cached, (r, got[r])
+        assert (why is None) == want, (r, why)
