@@ -76,9 +76,11 @@ const char *sgc_last_error(void);
  *                   (3 / 4: its diagnostic forms -- loads only / MFMAs only --
  *                   whose results are wrong by design);
  *   "linear_ck":    k per chunk of the streaming forward, 64 (default) or 32;
- *   "backward_kernel": classifier weight backward, 0 = auto (the fp32 MFMA
+ *   "backward_kernel": classifier weight backward, 0 = auto (split-bf16
+ *                   column blocks up to 48 classes, else the fp32 MFMA
  *                   slabs), 1 = fp32 MFMA slabs, 2 = split-bf16 slabs where X
- *                   gives 8-B lanes (K and ldx even).
+ *                   gives 8-B lanes (K and ldx even), 3 = split-bf16 column
+ *                   blocks (up to 48 classes; more: as 0).
  * sgc_get_tuning returns -1 for an unknown key. */
 int sgc_set_tuning(const char *key, int64_t value);
 int64_t sgc_get_tuning(const char *key);
@@ -413,8 +415,10 @@ int sgc_linear_f32(const float *X, int64_t ldx, const float *W, const float *b,
  * or invalid shape.  Static storage. */
 const char *sgc_linear_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C, const float *X);
 /* The weight-backward kernel sgc_linear_backward_f32 runs for this shape /
- * alignment (static string; bench labels). */
-const char *sgc_linear_backward_kernel_name(int64_t M, int64_t K, int64_t ldx, const float *X);
+ * alignment under the current "backward_kernel" tuning (static string; bench
+ * labels); "none" for an empty or invalid shape. */
+const char *sgc_linear_backward_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C,
+                                            const float *X);
 
 /* Backward of sgc_linear_f32 for the weights (what autograd runs for
  * nn.Linear after F.cross_entropy(model(x), y).backward() in the closures of

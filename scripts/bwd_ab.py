@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--features", type=int, default=602)
     ap.add_argument("--classes", type=int, default=41)
     ap.add_argument("--kernel", type=int, default=0,
-                    help="sgc_set_tuning('backward_kernel'): 0 auto, 1 fp32 slabs, 2 split-bf16")
+                    help="sgc_set_tuning('backward_kernel'): 0 auto, 1 fp32 slabs, 2 split-bf16 slabs, 3 split-bf16 column blocks")
     a = ap.parse_args()
     from sgc_amd import _lib
     _lib.check(_lib.load().sgc_set_tuning(b"backward_kernel", a.kernel), "set_tuning")
@@ -38,6 +38,7 @@ def main():
     refb = dy.double().sum(0)
     errb = ((db.cpu().double() - refb).abs().max() / refb.abs().max()).item()
     name = _lib.load().sgc_linear_backward_kernel_name(a.rows, a.features, xd.stride(0),
+                                                       a.classes,
                                                        _lib.ptr(xd)).decode()
     print(json.dumps({"lib": os.environ.get("SGC_AMD_LIB", "default"), "kernel": name,
                       "backward_ms": ms, "rel_err": err, "db_rel_err": errb}), flush=True)

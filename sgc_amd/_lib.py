@@ -69,7 +69,7 @@ SIGNATURES = {
     "sgc_launch_list_destroy": (ctypes.c_int, [_i64]),
     "sgc_linear_f32": (ctypes.c_int, [_p, _i64, _p, _p, _p, _i64, _i64, _i64, _i64, _p]),
     "sgc_linear_kernel_name": (ctypes.c_char_p, [_i64, _i64, _i64, _i64, _p]),
-    "sgc_linear_backward_kernel_name": (ctypes.c_char_p, [_i64, _i64, _i64, _p]),
+    "sgc_linear_backward_kernel_name": (ctypes.c_char_p, [_i64, _i64, _i64, _i64, _p]),
     "sgc_cross_entropy_workspace": (_i64, [_i64, _i64]),
     "sgc_cross_entropy_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i64, _p, _p, _p, _p, _i64,
                                              _p]),

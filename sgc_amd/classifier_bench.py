@@ -104,7 +104,9 @@ def classifier_record(dev, M=152410, K=602, C=41, reps=20, epochs=2, seed=0):
                       "torch_F_linear_ms": _median_ms(lambda: F.linear(x, W, b), reps, inner=10)}
     t = _median_ms(lambda: linear_backward(x, dY), reps, inner=10)
     t1 = _median_ms(lambda: linear_backward(x, dY), reps)
-    rec["backward"] = {"kernel": "xent_dw_kernel + reductions (sgc_linear_backward_f32)", "ms": t,
+    bname = _lib.load().sgc_linear_backward_kernel_name(M, K, x.stride(0), C, _lib.ptr(x)).decode()
+    rec["backward"] = {"kernel": f"{bname} + reduction (sgc_linear_backward_f32; name from "
+                                 "sgc_linear_backward_kernel_name)", "ms": t,
                        "single_call_ms": t1,
                        "bytes": bwd_bytes, "achieved_GBps": bwd_bytes / t / 1e6,
                        "frac": bwd_bytes / t / 1e6 / HBM_PEAK_GBS,

@@ -96,7 +96,8 @@ int propagate_cpu(const int32_t *row_ptr, const int32_t *col_idx, const float *v
                   int64_t n_rows, const float *X0, int64_t ldx, float *out, int64_t ldo, int64_t F,
                   int32_t K, void *workspace, int64_t workspace_bytes, int32_t n_threads);
 const char *linear_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C, const float *X);
-const char *linear_backward_kernel_name(int64_t M, int64_t K, int64_t ldx, const float *X);
+const char *linear_backward_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C,
+                                        const float *X);
 int launch_linear_f32(const float *X, int64_t ldx, const float *W, const float *b, float *Y,
                       int64_t ldy, int64_t M, int64_t K, int64_t C, hipStream_t stream);
 int64_t plan_sorted_workspace(int64_t n_rows);
@@ -507,8 +508,9 @@ const char *sgc_linear_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C,
     return linear_kernel_name(M, K, ldx, C, X);
 }
 
-const char *sgc_linear_backward_kernel_name(int64_t M, int64_t K, int64_t ldx, const float *X) {
-    return linear_backward_kernel_name(M, K, ldx, X);
+const char *sgc_linear_backward_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C,
+                                            const float *X) {
+    return linear_backward_kernel_name(M, K, ldx, C, X);
 }
 
 int64_t sgc_linear_backward_workspace(int64_t M, int64_t K, int64_t C) {

@@ -1723,7 +1723,7 @@ int set_tuning(const char *key, int64_t value) {
         return SGC_OK;
     }
     if (std::string(key) == "backward_kernel") {
-        SGC_REQUIRE(value >= 0 && value <= 2, SGC_EINVAL, "backward_kernel must be 0..2");
+        SGC_REQUIRE(value >= 0 && value <= 3, SGC_EINVAL, "backward_kernel must be 0..3");
         g_backward_kernel = (int)value;
         return SGC_OK;
     }

@@ -464,6 +464,221 @@ __global__ __launch_bounds__(256) void xent_dw_split_kernel(
     }
 }
 
+// NT consecutive floats at byte offset off (one 4-, 8- or 12-B buffer load;
+// past the range: 0 per dword)
+template <int NT>
+__device__ __forceinline__ void buffer_load_floats(__amdgpu_buffer_rsrc_t r, uint32_t off,
+                                                   float (&v)[NT]) {
+    static_assert(NT >= 1 && NT <= 3, "1-3 floats");
+    if constexpr (NT == 3) {
+        typedef float f3 __attribute__((ext_vector_type(3)));
+        const f3 x = __builtin_bit_cast(f3, __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, 0));
+        v[0] = x[0];
+        v[1] = x[1];
+        v[2] = x[2];
+    } else if constexpr (NT == 2) {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 x = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+        v[0] = x[0];
+        v[1] = x[1];
+    } else {
+        v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+    }
+}
+
+// ---- B'': dW on split-bf16 products over column blocks (round 6) -----------
+// What B and B' spend besides the stream: a C16 x K partial per 224-300-row
+// slab -- 512-681 partials, 59-79 MB written and read back by the reduction,
+// a fifth of the algorithmic bytes -- and for B' 1.33 rounds of blocks.  Here a
+// block owns a 64-column block cb of X and a row range r (R ranges: R x
+// ceil(K / 64) blocks, one round at two blocks per CU).  Its four waves stream
+// contiguous quarters of the range, 32 rows a step; lane (g, i) reads
+//   dY rows 32s + 8g + t (t < 8), classes NT i .. NT i + NT - 1 (one 4-, 8- or
+//      12-B load per row): row i of class tile n is class NT i + n, so a
+//      lane's classes are adjacent in dY's row (8 loads a step, not 8 NT),
+//      the A operands of the NT tiles, and
+//   X rows 32s + 8g + t, columns c0 + 4i .. c0 + 4i + 3 (16-B loads; 4 rows
+//      x 256 B per instruction): the B operands of N-tiles e = 0..3 (column
+//      c0 + 4i + e), no lane exchange,
+// splits both into three bf16 pieces (split_bf16.h) and runs NT x 4 x 6
+// v_mfma_f32_16x16x32_bf16, the next step's loads in flight.  The waves'
+// accumulators are summed in LDS in wave order and the block stores its 64
+// columns of partial r: R partials in all (48 at the Reddit-train shape:
+// 4.7 MB).  dY is read by each column block of a range; block b runs on XCD
+// b % 8, and the blocks of range r are numbered so b % 8 == r % 8: a range's
+// ten dY reads share one L2.  Columns past K read whatever lies there (the
+// next row, or 0 past the range) and are never stored: column j of dW
+// depends on column j of X only.
+#ifndef SGC_DW_COL_RANGES
+#define SGC_DW_COL_RANGES 48
+#endif
+constexpr int kDwColRanges = SGC_DW_COL_RANGES;  // row ranges (a multiple of 8: the XCD numbering)
+constexpr int kDwColWidth = 64;   // columns per block
+
+template <int NT>
+__global__ __launch_bounds__(256) void xent_dw_cols_kernel(
+    const float *__restrict__ X, int64_t ldx, const float *__restrict__ G, int ldg, int M, int K,
+    int C, int n_cblk, int R, float *__restrict__ slab, float *__restrict__ db_slab) {
+    __shared__ f32x4 red[4][NT][4][64];  // [wave][class tile][q][lane] -> N-tiles e = 0..3
+    __shared__ float dbr[4][NT * 16];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform loop bounds
+    const int i = lane & 15, g = lane >> 4;
+    const int q8 = (int)blockIdx.x >> 3;
+    const int cb = q8 % n_cblk, r = (q8 / n_cblk) * 8 + ((int)blockIdx.x & 7);
+    if (r >= R) return;  // (uniform per block: no barrier reached)
+    const int S = (M + 31) >> 5;
+    const int s_a = (int)((int64_t)S * r / R), s_b = (int)((int64_t)S * (r + 1) / R);
+    const int row_a = 32 * s_a;
+    const int n_rows = max(0, min(M, 32 * s_b) - row_a);
+    const int ns = s_b - s_a;
+    const int w_a = ns * w / 4, w_b = ns * (w + 1) / 4;  // this wave's steps, block-relative
+    const int c0 = cb * kDwColWidth;
+    const auto xdsc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(X + (int64_t)row_a * ldx), 0,
+        n_rows ? (int)(((int64_t)(n_rows - 1) * ldx + K) * 4) : 0, 0x00020000);
+    const auto gdsc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(G + (int64_t)row_a * ldg), 0,
+        n_rows ? (int)(((int64_t)(n_rows - 1) * ldg + C) * 4) : 0, 0x00020000);
+    const uint32_t xpitch = (uint32_t)ldx * 4u, gpitch = (uint32_t)ldg * 4u;
+    const uint32_t xlane = (uint32_t)(8 * g * ldx + c0 + 4 * i) * 4u;
+    // classes NT i + n; a lane whose first class is past C reads nothing (a
+    // partly valid lane reads classes past C from the next row or as 0: they
+    // reach only rows of dW past C, never stored)
+    const uint32_t glane = NT * i < C ? (uint32_t)(8 * g * ldg + NT * i) * 4u : kOffOOB;
+    f32x4 xr[8];
+    float gr[8][NT];
+    // every load issued on every path (hipcc's counted waits stay exact); a
+    // step past the wave's range reads out-of-range offsets: 0, no traffic
+    auto load = [&](int st) {
+        const bool live = st < w_b;
+        const uint32_t rx = live ? xlane + (uint32_t)st * 32u * xpitch : kOffOOB;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            xr[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  xdsc, rx + (uint32_t)t * xpitch, 0, 0));
+        const uint32_t rg = live ? glane + (uint32_t)st * 32u * gpitch : kOffOOB;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) buffer_load_floats<NT>(gdsc, rg + (uint32_t)t * gpitch, gr[t]);
+    };
+    // hh products in accH, the five small ones in accL (as the forward)
+    f32x4 accH[NT][4], accL[NT][4];
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            accH[n][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+            accL[n][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    const bool sum_db = db_slab && cb == 0;  // column block 0 also sums dY's rows
+    float dba[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) dba[n] = 0.f;
+    load(w_a);
+    for (int st = w_a; st < w_b; ++st) {
+        u32x4 ga[NT][3], xb[4][3];
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t h, m, lo;
+                split3(gr[2 * q][n], gr[2 * q + 1][n], h, m, lo);
+                ga[n][0][q] = h;
+                ga[n][1][q] = m;
+                ga[n][2][q] = lo;
+            }
+        if (sum_db) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+#pragma unroll
+                for (int t = 0; t < 8; ++t) dba[n] += gr[t][n];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t h, m, lo;
+                split3(xr[2 * q][e], xr[2 * q + 1][e], h, m, lo);
+                xb[e][0][q] = h;
+                xb[e][1][q] = m;
+                xb[e][2][q] = lo;
+            }
+        load(st + 1);
+        // the next step's loads go out before this step's MFMAs (the
+        // scheduler otherwise interleaves the splits with the MFMAs and
+        // issues the loads two thirds of the way through them)
+        __builtin_amdgcn_sched_barrier(0);
+#if defined(SGC_DW_COLS_DIAG) && SGC_DW_COLS_DIAG == 1  // measurement: loads only
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) accH[0][e][t & 3] += xr[t][e] + gr[t][e % NT];
+        continue;
+#elif defined(SGC_DW_COLS_DIAG) && SGC_DW_COLS_DIAG == 2  // measurement: loads + splits
+        uint32_t fold = 0;
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) fold ^= xb[e][p][q];
+#pragma unroll
+                for (int n = 0; n < NT; ++n) fold ^= ga[n][p][q];
+            }
+        accH[0][0][0] += __uint_as_float(fold & 0x807fffffu);
+        continue;
+#endif
+        auto A = [&](int n, int p) { return __builtin_bit_cast(bf16x8_t, ga[n][p]); };
+        auto B = [&](int e, int p) { return __builtin_bit_cast(bf16x8_t, xb[e][p]); };
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+                accH[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 0), B(e, 0), accH[n][e], 0, 0, 0);
+                accL[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 0), B(e, 1), accL[n][e], 0, 0, 0);
+                accL[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 1), B(e, 0), accL[n][e], 0, 0, 0);
+                accL[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 0), B(e, 2), accL[n][e], 0, 0, 0);
+                accL[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 2), B(e, 0), accL[n][e], 0, 0, 0);
+                accL[n][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A(n, 1), B(e, 1), accL[n][e], 0, 0, 0);
+            }
+    }
+    // D[row 4g + q][j = i] of tile (n, e) -> class NT (4g + q) + n, column c0 + 4i + e
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            red[w][n][q][lane] = f32x4{accH[n][0][q] + accL[n][0][q], accH[n][1][q] + accL[n][1][q],
+                                       accH[n][2][q] + accL[n][2][q], accH[n][3][q] + accL[n][3][q]};
+    if (sum_db) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+            float v = dba[n];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            if (g == 0) dbr[w][NT * i + n] = v;
+        }
+    }
+    __syncthreads();
+    // the block's partial: classes < C x its columns < K, the waves in order;
+    // thread (cls = NT (4 gg + q) + n, col): red[.][n][q][16 gg + ii][e] is
+    // float 64 gg + col of row (n, q)
+    const int col = threadIdx.x & 63;
+    const float *rf = reinterpret_cast<const float *>(red);
+    float *out = slab + (int64_t)r * (NT * 16) * K;
+    if (c0 + col < K) {
+        for (int cls = threadIdx.x >> 6; cls < C; cls += 4) {
+            const int r4 = cls / NT, n = cls - r4 * NT, gg = r4 >> 2, q = r4 & 3;
+            const int at = ((n * 4 + q) * 64) * 4 + 64 * gg + col;
+            constexpr int wstride = NT * 4 * 64 * 4;
+            out[(int64_t)cls * K + c0 + col] =
+                ((rf[at] + rf[at + wstride]) + rf[at + 2 * wstride]) + rf[at + 3 * wstride];
+        }
+    }
+    if (sum_db && (int)threadIdx.x < C)
+        db_slab[(int64_t)r * (NT * 16) + threadIdx.x] =
+            ((dbr[0][threadIdx.x] + dbr[1][threadIdx.x]) + dbr[2][threadIdx.x]) + dbr[3][threadIdx.x];
+}
+
 // ---- C: fixed-order reductions ----------------------------------------------
 // dW: a block owns 64 consecutive elements; wave w sums slabs [w*n/4, (w+1)*n/4)
 // in order (coalesced 256-B rows of each slab), then wave 0 adds the four
@@ -516,15 +731,15 @@ __global__ __launch_bounds__(256) void xent_reduce_dw_db_kernel(
             const int64_t cls = e / K, k = e - cls * K;
             const float *p = slab + cls * K + k;
             const int64_t stride = (int64_t)C16 * K;
-            int j = j0;
-            for (; j + 8 <= j1; j += 8) {
-                float v[8];
+            // 16 loads in flight per batch (the column-block kernel's 48
+            // partials: one batch per wave; a slot past j1 adds 0)
+            for (int j = j0; j < j1; j += 16) {
+                float v[16];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(j + u) * stride];
+                for (int u = 0; u < 16; ++u) v[u] = j + u < j1 ? p[(int64_t)(j + u) * stride] : 0.f;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) s += v[u];
+                for (int u = 0; u < 16; ++u) s += v[u];
             }
-            for (; j < j1; ++j) s += p[(int64_t)j * stride];
         }
     } else {
         // db: one wave per class -- lane l sums slabs l, l + 64, ... (eight
@@ -618,15 +833,37 @@ hipError_t launch_dw_split(const float *X, int64_t ldx, const float *G, int ldg,
     return hipGetLastError();
 }
 
+// Row ranges of xent_dw_cols_kernel: kDwColRanges, fewer when M has fewer
+// 32-row steps.
+inline int dw_col_ranges(int64_t M) {
+    return (int)std::min<int64_t>(kDwColRanges, std::max<int64_t>(1, (M + 31) / 32));
+}
+
+template <int NT>
+hipError_t launch_dw_cols(const float *X, int64_t ldx, const float *G, int ldg, int M, int K,
+                          int C, float *slab, float *db_slab, hipStream_t s) {
+    const int R = dw_col_ranges(M);
+    const int n_cblk = (K + kDwColWidth - 1) / kDwColWidth;
+    const int blocks = n_cblk * ((R + 7) / 8) * 8;
+    hipLaunchKernelGGL((xent_dw_cols_kernel<NT>), dim3(blocks), dim3(256), 0, s, X, ldx, G, ldg, M,
+                       K, C, n_cblk, R, slab, db_slab);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 // Backward kernel choice (sgc_set_tuning("backward_kernel")): 0 auto (the
-// fp32 MFMA slabs: the split form measured slower, see xent_dw_split_kernel),
-// 1 the fp32 MFMA slabs, 2 the split-bf16 slabs where X gives 8-B lanes.
+// split-bf16 column blocks up to 48 classes, the fp32 MFMA slabs above), 1 the
+// fp32 MFMA slabs, 2 the split-bf16 slabs where X gives 8-B lanes, 3 the
+// split-bf16 column blocks (up to 48 classes).
 int g_backward_kernel = 0;
 
 static bool backward_split(int64_t K, int64_t ldx, const float *X) {
     return g_backward_kernel == 2 && K % 2 == 0 && ldx % 2 == 0 && (uintptr_t)X % 8 == 0;
+}
+
+static bool backward_cols(int64_t C) {
+    return (g_backward_kernel == 0 || g_backward_kernel == 3) && C <= 48;
 }
 
 int64_t xent_workspace_bytes(int64_t M, int64_t K, int64_t C) {
@@ -732,8 +969,10 @@ int64_t linear_backward_workspace_bytes(int64_t M, int64_t K, int64_t C) {
     const int64_t C16 = (C + 15) / 16 * 16;
     // the larger of the two kernels' slab counts (fp32: <= kDwSlabs slabs;
     // split-bf16: kDwSplitRows rows each)
-    const int64_t n_slabs = std::max<int64_t>(std::min<int64_t>(kDwSlabs, (M + 255) / 256),
-                                              (M + kDwSplitRows - 1) / kDwSplitRows);
+    const int64_t n_slabs = std::max<int64_t>(
+        std::max<int64_t>(std::min<int64_t>(kDwSlabs, (M + 255) / 256),
+                          (M + kDwSplitRows - 1) / kDwSplitRows),
+        dw_col_ranges(M));
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     return al(n_slabs * C16 * K * 4) + al(n_slabs * C16 * 4) + 512;
 }
@@ -764,8 +1003,10 @@ int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ld
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     char *p = (char *)(((uintptr_t)ws + 255) & ~uintptr_t(255));
     float *slab = (float *)p;
-    p += al((int64_t)std::max<int64_t>(max_slabs, (M + kDwSplitRows - 1) / kDwSplitRows) * C16 *
-            K * 4);
+    p += al((int64_t)std::max<int64_t>(
+                std::max<int64_t>(max_slabs, (M + kDwSplitRows - 1) / kDwSplitRows),
+                dw_col_ranges(M)) *
+            C16 * K * 4);
     float *db_slab = db ? (float *)p : nullptr;
     int V = 1;
     for (int v : {4, 2})
@@ -774,7 +1015,24 @@ int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ld
             break;
         }
     hipError_t e = hipSuccess;
-    if (split) {
+    const bool cols = backward_cols(C);
+    int n_parts = n_slabs;
+    if (cols) {
+        const int R = dw_col_ranges(M);
+        const int64_t steps = ((M + 31) / 32 + R - 1) / R;
+        SGC_REQUIRE(dw_slab_fits(32 * steps, ldx, ldd), SGC_ERANGE,
+                    "classifier dW: %lld rows x ldx %lld past the kernel's 31-bit offsets",
+                    (long long)(32 * steps), (long long)ldx);
+        n_parts = R;
+        switch (NT) {
+            case 1: e = launch_dw_cols<1>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, slab,
+                                          db_slab, s); break;
+            case 2: e = launch_dw_cols<2>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, slab,
+                                          db_slab, s); break;
+            default: e = launch_dw_cols<3>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, slab,
+                                           db_slab, s); break;
+        }
+    } else if (split) {
         switch (NT) {
             case 1: e = launch_dw_split<1>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, n_slabs,
                                            rows_per, slab, db_slab, s); break;
@@ -812,15 +1070,18 @@ int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ld
     const int dw_blocks = (int)((C * K + 63) / 64);
     const int db_blocks = db ? (int)((C + 3) / 4) : 0;  // a wave per class
     hipLaunchKernelGGL(xent_reduce_dw_db_kernel, dim3((unsigned)(dw_blocks + db_blocks)),
-                       dim3(256), 0, s, slab, n_slabs, (int)C, (int)K, C16, dW, db_slab, db,
+                       dim3(256), 0, s, slab, n_parts, (int)C, (int)K, C16, dW, db_slab, db,
                        dw_blocks);
     SGC_HIP_CHECK(hipGetLastError());
     return SGC_OK;
 }
 
-const char *linear_backward_kernel_name(int64_t M, int64_t K, int64_t ldx, const float *X) {
-    if (M <= 0 || K <= 0 || ldx < K) return "none";
+const char *linear_backward_kernel_name(int64_t M, int64_t K, int64_t ldx, int64_t C,
+                                        const float *X) {
+    if (M <= 0 || K <= 0 || C <= 0 || C > 64 || ldx < K) return "none";
     const bool split = backward_split(K, ldx, X);
+    if (backward_cols(C))
+        return "xent_dw_cols_kernel (split-bf16 column blocks, v_mfma_f32_16x16x32_bf16 x 6 products)";
     return split ? "xent_dw_split_kernel (split-bf16 slabs, v_mfma_f32_16x16x32_bf16 x 6 products)"
                  : "xent_dw_kernel (fp32 slabs, v_mfma_f32_16x16x4_f32)";
 }

@@ -852,24 +852,36 @@ def test_sgc_model_autograd_matches_torch():
     assert isinstance(get_model("SGC", 10, 3, cuda=True), SGC)
 
 
-@pytest.mark.parametrize("kernel", [0, 2])
+def _backward_kernel_expected(kernel, K, C):
+    if kernel in (0, 3) and C <= 48:
+        return "xent_dw_cols"
+    if kernel == 2 and K % 2 == 0:
+        return "xent_dw_split"
+    return "xent_dw_kernel"
+
+
+@pytest.mark.parametrize("kernel", [0, 1, 2])
 @pytest.mark.parametrize("M,K,C", [(1, 3, 2), (140, 1433, 7), (333, 602, 41), (1000, 500, 3),
                                    (4099, 602, 41), (77, 64, 64), (600, 130, 17), (152410, 602, 41),
-                                   (5, 601, 1), (225, 34, 48), (100000, 602, 41)])
+                                   (5, 601, 1), (225, 34, 48), (100000, 602, 41), (31, 65, 33),
+                                   (1537, 129, 16), (20000, 602, 49)])
 def test_linear_backward_matches_torch(M, K, C, kernel, request):
     """sgc_linear_backward_f32 (the SGC.forward backward: dW = dY^T X, db =
     sum dY from one read of X) vs fp64 torch, fp32 tolerance; dY a caller's
     [M, C] tensor (classes not a multiple of 16 are masked in the kernel);
-    bitwise reproducible run to run.  kernel 2 forces the split-bf16 slabs
-    (xent_dw_split_kernel: ragged last slab and 32-row step, K not a multiple
-    of 32, one to four class tiles; odd K falls back to the fp32 slabs)."""
+    bitwise reproducible run to run.  kernel 0 (auto) takes the split-bf16
+    column blocks up to 48 classes (xent_dw_cols_kernel: fewer 32-row steps
+    than row ranges, a ragged last step, K not a multiple of 64 or of 4, one
+    to three class tiles) and the fp32 slabs above; 1 forces the fp32 slabs;
+    2 the split-bf16 slabs (xent_dw_split_kernel; odd K falls back to the
+    fp32 slabs)."""
     from sgc_amd import _lib
     from sgc_amd.propagate import linear_backward
     lib = _lib.load()
     _lib.check(lib.sgc_set_tuning(b"backward_kernel", kernel), "set_tuning")
     request.addfinalizer(lambda: lib.sgc_set_tuning(b"backward_kernel", 0))
-    name = lib.sgc_linear_backward_kernel_name(M, K, K, None).decode()
-    assert name.startswith("xent_dw_split" if kernel == 2 and K % 2 == 0 else "xent_dw_kernel"), name
+    name = lib.sgc_linear_backward_kernel_name(M, K, K, C, None).decode()
+    assert name.startswith(_backward_kernel_expected(kernel, K, C)), name
     g = torch.Generator().manual_seed(M + 3 * K + C)
     X = torch.randn((M, K), generator=g)
     dY = torch.randn((M, C), generator=g) / M
@@ -884,6 +896,45 @@ def test_linear_backward_matches_torch(M, K, C, kernel, request):
     assert torch.equal(dW, dW2) and torch.equal(db, db2)
     dW3, none = linear_backward(X.to(DEV), dY.to(DEV), want_bias=False)
     assert none is None and torch.equal(dW, dW3)
+
+
+@pytest.mark.parametrize("M", [33, 1000, 152410])
+def test_linear_backward_cols_edges(M):
+    """The column-block backward's edges, each isolated so one element
+    would show: (1) dY zero but for the LAST row, K = 602 (the 16-B lane of
+    columns 600..603 straddles the end of X: columns 600, 601 must still
+    read), so dW must be that row's outer product; (2) X a column slice of a
+    wider tensor whose padding columns hold NaN and dY a class slice whose
+    padding holds NaN -- the padding is read into columns never stored, or not
+    read at all, and no NaN may reach dW or db."""
+    from sgc_amd.propagate import linear_backward
+    g = torch.Generator().manual_seed(M)
+    K, C = 602, 41
+    X = torch.randn((M, K), generator=g)
+    dY = torch.zeros((M, C))
+    dY[-1] = torch.randn(C, generator=g)
+    name = _lib_load().sgc_linear_backward_kernel_name(M, K, K, C, None).decode()
+    assert name.startswith("xent_dw_cols"), name
+    dW, db = linear_backward(X.to(DEV), dY.to(DEV))
+    want = dY[-1].double()[:, None] * X[-1].double()[None, :]
+    torch.testing.assert_close(dW.cpu().double(), want, rtol=1e-6, atol=0)
+    assert torch.equal(db.cpu(), dY[-1])
+    Xw = torch.full((M, 640), float("nan"))
+    Xw[:, :K] = torch.randn((M, K), generator=g)
+    dYw = torch.full((M, 48), float("nan"))
+    dYw[:, :C] = torch.randn((M, C), generator=g) / M
+    dW, db = linear_backward(Xw.to(DEV)[:, :K], dYw.to(DEV)[:, :C])
+    assert torch.isfinite(dW).all() and torch.isfinite(db).all()
+    wref = dYw[:, :C].double().t() @ Xw[:, :K].double()
+    torch.testing.assert_close(dW.cpu().double(), wref, rtol=1e-4,
+                               atol=1e-5 * wref.abs().max().item())
+    torch.testing.assert_close(db.cpu().double(), dYw[:, :C].double().sum(0), rtol=1e-4,
+                               atol=1e-6)
+
+
+def _lib_load():
+    from sgc_amd import _lib
+    return _lib.load()
 
 
 @pytest.mark.parametrize("M,K,C", [(1, 3, 2), (140, 1433, 7), (333, 602, 41), (1000, 500, 3),
