@@ -490,9 +490,13 @@ __device__ __forceinline__ void buffer_load_floats(__amdgpu_buffer_rsrc_t r, uin
 // What B and B' spend besides the stream: a C16 x K partial per 224-300-row
 // slab -- 512-681 partials, 59-79 MB written and read back by the reduction,
 // a fifth of the algorithmic bytes -- and for B' 1.33 rounds of blocks.  Here a
-// block owns a 64-column block cb of X and a row range r (R ranges: R x
-// ceil(K / 64) blocks, one round at two blocks per CU).  Its four waves stream
-// contiguous quarters of the range, 32 rows a step; lane (g, i) reads
+// block owns a 64-column block cb of X and a row "range" r (R ranges: R x
+// ceil(K / 64) blocks, one round at two blocks per CU).  Range r is the
+// 32-row steps r, r + R, r + 2R, ... and the block's wave w takes every fourth
+// of them, so at any moment the grid reads X inside a window of ~4R steps
+// (contiguous ranges, 48 separate runs: loads alone 78 vs 76 us, whole kernel
+// 1-2 us slower, profiles/r06/s18); a step's own descriptors bound it (rows
+// past M read 0).  Per step lane (g, i) reads
 //   dY rows 32s + 8g + t (t < 8), classes NT i .. NT i + NT - 1 (one 4-, 8- or
 //      12-B load per row): row i of class tile n is class NT i + n, so a
 //      lane's classes are adjacent in dY's row (8 loads a step, not 8 NT),
@@ -507,7 +511,7 @@ __device__ __forceinline__ void buffer_load_floats(__amdgpu_buffer_rsrc_t r, uin
 // 4.7 MB).  dY is read by each column block of a range; block b runs on XCD
 // b % 8, and the blocks of range r are numbered so b % 8 == r % 8: a range's
 // ten dY reads share one L2.  Columns past K read whatever lies there (the
-// next row, or 0 past the range) and are never stored: column j of dW
+// next row, or 0 past the step) and are never stored: column j of dW
 // depends on column j of X only.
 #ifndef SGC_DW_COL_RANGES
 #define SGC_DW_COL_RANGES 48
@@ -528,38 +532,42 @@ __global__ __launch_bounds__(256) void xent_dw_cols_kernel(
     const int cb = q8 % n_cblk, r = (q8 / n_cblk) * 8 + ((int)blockIdx.x & 7);
     if (r >= R) return;  // (uniform per block: no barrier reached)
     const int S = (M + 31) >> 5;
-    const int s_a = (int)((int64_t)S * r / R), s_b = (int)((int64_t)S * (r + 1) / R);
-    const int row_a = 32 * s_a;
-    const int n_rows = max(0, min(M, 32 * s_b) - row_a);
-    const int ns = s_b - s_a;
-    const int w_a = ns * w / 4, w_b = ns * (w + 1) / 4;  // this wave's steps, block-relative
     const int c0 = cb * kDwColWidth;
-    const auto xdsc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(X + (int64_t)row_a * ldx), 0,
-        n_rows ? (int)(((int64_t)(n_rows - 1) * ldx + K) * 4) : 0, 0x00020000);
-    const auto gdsc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float *>(G + (int64_t)row_a * ldg), 0,
-        n_rows ? (int)(((int64_t)(n_rows - 1) * ldg + C) * 4) : 0, 0x00020000);
     const uint32_t xpitch = (uint32_t)ldx * 4u, gpitch = (uint32_t)ldg * 4u;
-    const uint32_t xlane = (uint32_t)(8 * g * ldx + c0 + 4 * i) * 4u;
+    // a lane whose four columns all lie past K reads nothing (the last block's
+    // lanes would otherwise read the next row's first columns)
+    const uint32_t xlane = c0 + 4 * i < K ? (uint32_t)(8 * g * ldx + c0 + 4 * i) * 4u : kOffOOB;
     // classes NT i + n; a lane whose first class is past C reads nothing (a
     // partly valid lane reads classes past C from the next row or as 0: they
     // reach only rows of dW past C, never stored)
     const uint32_t glane = NT * i < C ? (uint32_t)(8 * g * ldg + NT * i) * 4u : kOffOOB;
     f32x4 xr[8];
     float gr[8][NT];
-    // every load issued on every path (hipcc's counted waits stay exact); a
-    // step past the wave's range reads out-of-range offsets: 0, no traffic
-    auto load = [&](int st) {
-        const bool live = st < w_b;
-        const uint32_t rx = live ? xlane + (uint32_t)st * 32u * xpitch : kOffOOB;
+    // range r's steps are r, r + R, r + 2R, ... and wave w takes every fourth
+    // of them: at any moment the whole grid reads inside a window of ~4R
+    // steps of X, not R separate runs; a step's own descriptors (rows past M,
+    // and steps past the last, read 0)
+    const int w_a = w, w_b = (S - r + R - 1) / R, w_step = 4;
+    auto load = [&](int j) {
+        const int s = r + R * j;
+        const int rows = s < S ? min(32, M - 32 * s) : 0;
+        const int64_t row0 = s < S ? 32 * (int64_t)s : 0;
+        const auto xd = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float *>(X + row0 * ldx), 0, rows ? (int)(((int64_t)(rows - 1) * ldx + K) * 4) : 0,
+            0x00020000);
+        const auto gd = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float *>(G + row0 * ldg), 0, rows ? (int)(((int64_t)(rows - 1) * ldg + C) * 4) : 0,
+            0x00020000);
+        // (the lane offsets opaque per step: hoisted, the 16 row offsets would
+        // hold 16 VGPRs for the whole loop and cost the second wave per SIMD)
+        uint32_t xl = xlane, gl = glane;
+        asm volatile("" : "+v"(xl), "+v"(gl));
 #pragma unroll
         for (int t = 0; t < 8; ++t)
             xr[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  xdsc, rx + (uint32_t)t * xpitch, 0, 0));
-        const uint32_t rg = live ? glane + (uint32_t)st * 32u * gpitch : kOffOOB;
+                                                  xd, xl + (uint32_t)t * xpitch, 0, 0));
 #pragma unroll
-        for (int t = 0; t < 8; ++t) buffer_load_floats<NT>(gdsc, rg + (uint32_t)t * gpitch, gr[t]);
+        for (int t = 0; t < 8; ++t) buffer_load_floats<NT>(gd, gl + (uint32_t)t * gpitch, gr[t]);
     };
     // hh products in accH, the five small ones in accL (as the forward)
     f32x4 accH[NT][4], accL[NT][4];
@@ -575,7 +583,7 @@ __global__ __launch_bounds__(256) void xent_dw_cols_kernel(
 #pragma unroll
     for (int n = 0; n < NT; ++n) dba[n] = 0.f;
     load(w_a);
-    for (int st = w_a; st < w_b; ++st) {
+    for (int st = w_a; st < w_b; st += w_step) {
         u32x4 ga[NT][3], xb[4][3];
 #pragma unroll
         for (int n = 0; n < NT; ++n)
@@ -603,7 +611,7 @@ __global__ __launch_bounds__(256) void xent_dw_cols_kernel(
                 xb[e][1][q] = m;
                 xb[e][2][q] = lo;
             }
-        load(st + 1);
+        load(st + w_step);
         // the next step's loads go out before this step's MFMAs (the
         // scheduler otherwise interleaves the splits with the MFMAs and
         // issues the loads two thirds of the way through them)
@@ -1018,12 +1026,11 @@ int linear_backward_f32(const float *X, int64_t ldx, const float *dY, int64_t ld
     const bool cols = backward_cols(C);
     int n_parts = n_slabs;
     if (cols) {
-        const int R = dw_col_ranges(M);
-        const int64_t steps = ((M + 31) / 32 + R - 1) / R;
-        SGC_REQUIRE(dw_slab_fits(32 * steps, ldx, ldd), SGC_ERANGE,
-                    "classifier dW: %lld rows x ldx %lld past the kernel's 31-bit offsets",
-                    (long long)(32 * steps), (long long)ldx);
-        n_parts = R;
+        // a step's 32 rows are one descriptor's range
+        SGC_REQUIRE(dw_slab_fits(32, ldx, ldd), SGC_ERANGE,
+                    "classifier dW: 32 rows x ldx %lld past the kernel's 31-bit offsets",
+                    (long long)ldx);
+        n_parts = dw_col_ranges(M);
         switch (NT) {
             case 1: e = launch_dw_cols<1>(X, ldx, dY, (int)ldd, (int)M, (int)K, (int)C, slab,
                                           db_slab, s); break;
