@@ -10,8 +10,10 @@
 //                         row softmax / log-sum-exp across the 16-lane class
 //                         groups (DPP shuffles), G -> global [M][C16] (fp32,
 //                         padded classes 0), per-wave loss and dG column sums;
-//   B  xent_dw_kernel     dW partial slabs: each block owns a contiguous run
-//                         of rows and reduces G^T X over them on MFMA
+//   B  xent_dw_cols_kernel (up to 48 classes; round 6) dW partials over
+//                         column blocks x row ranges on split-bf16 MFMA, or
+//                         xent_dw_kernel: dW partial slabs, each block a
+//                         contiguous run of rows reduced on fp32 MFMA
 //                         (A = G^T straight from G's row-major layout,
 //                         B = X rows, V-vector loads split over V MFMAs);
 //   C  xent_reduce_kernel slabs -> dW, per-wave partials -> db and loss, in a
@@ -878,7 +880,9 @@ int64_t xent_workspace_bytes(int64_t M, int64_t K, int64_t C) {
     if (M <= 0 || K <= 0 || C <= 0) return 0;
     const int64_t C16 = (C + 15) / 16 * 16;
     const int64_t waves = (M + kLdsBM - 1) / kLdsBM * 4;
-    const int64_t n_slabs = std::min<int64_t>(kDwSlabs, (M + 255) / 256);
+    // dW partials: the fp32 slabs' or the column blocks' row ranges
+    const int64_t n_slabs = std::max<int64_t>(std::min<int64_t>(kDwSlabs, (M + 255) / 256),
+                                              dw_col_ranges(M));
     auto al = [](int64_t x) { return (x + 255) / 256 * 256; };
     return al(M * C16 * 4) + al(waves * 8) + al(waves * C16 * 4) + al(n_slabs * C16 * K * 4) + 512;
 }
@@ -917,6 +921,9 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
     p += al((int64_t)waves * C16 * 4);
     float *slab = (float *)p;
 
+    // dW on the split-bf16 column blocks up to 48 classes (as the backward)
+    const bool cols = backward_cols(C) && dw_slab_fits(32, ldx, C16);
+    const int n_parts = cols ? dw_col_ranges(M) : n_slabs;
     int V = 1;
     for (int v : {4, 2})
         if (K % v == 0 && ldx % v == 0 && (uintptr_t)X % (4 * v) == 0 && (uintptr_t)W % (4 * v) == 0) {
@@ -928,18 +935,24 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
     switch (NT) {                                                                                \
         case 1: e = launch_fwd<VV, 1>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,      \
                                       loss_part, db_part, logits, ldl, s);                       \
-            if (e == hipSuccess) e = launch_dw<VV, 1>(X, ldx, G, C16, (int)M, (int)K, C16,    \
-                                                      n_slabs, rows_per, slab, nullptr, s);                        \
+            if (e == hipSuccess)                                                                 \
+                e = cols ? launch_dw_cols<1>(X, ldx, G, C16, (int)M, (int)K, (int)C, slab, nullptr, s) \
+                         : launch_dw<VV, 1>(X, ldx, G, C16, (int)M, (int)K, C16, n_slabs, rows_per,   \
+                                              slab, nullptr, s);                                        \
             break;                                                                               \
         case 2: e = launch_fwd<VV, 2>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,      \
                                       loss_part, db_part, logits, ldl, s);                       \
-            if (e == hipSuccess) e = launch_dw<VV, 2>(X, ldx, G, C16, (int)M, (int)K, C16,    \
-                                                      n_slabs, rows_per, slab, nullptr, s);                        \
+            if (e == hipSuccess)                                                                 \
+                e = cols ? launch_dw_cols<2>(X, ldx, G, C16, (int)M, (int)K, (int)C, slab, nullptr, s) \
+                         : launch_dw<VV, 2>(X, ldx, G, C16, (int)M, (int)K, C16, n_slabs, rows_per,   \
+                                              slab, nullptr, s);                                        \
             break;                                                                               \
         case 3: e = launch_fwd<VV, 3>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,      \
                                       loss_part, db_part, logits, ldl, s);                       \
-            if (e == hipSuccess) e = launch_dw<VV, 3>(X, ldx, G, C16, (int)M, (int)K, C16,    \
-                                                      n_slabs, rows_per, slab, nullptr, s);                        \
+            if (e == hipSuccess)                                                                 \
+                e = cols ? launch_dw_cols<3>(X, ldx, G, C16, (int)M, (int)K, (int)C, slab, nullptr, s) \
+                         : launch_dw<VV, 3>(X, ldx, G, C16, (int)M, (int)K, C16, n_slabs, rows_per,   \
+                                              slab, nullptr, s);                                        \
             break;                                                                               \
         default: e = launch_fwd<VV, 4>(X, ldx, W, b, labels, (int)M, (int)K, (int)C, G, C16,     \
                                        loss_part, db_part, logits, ldl, s);                      \
@@ -958,7 +971,7 @@ int linear_xent_f32(const float *X, int64_t ldx, const float *W, const float *b,
     SGC_REQUIRE(e == hipSuccess, SGC_EHIP, "linear_xent launch failed: %s", hipGetErrorString(e));
     const int64_t ck = C * K;
     hipLaunchKernelGGL(xent_reduce_dw_kernel, dim3((unsigned)((ck + 63) / 64)), dim3(256), 0, s,
-                       slab, n_slabs, (int)C, (int)K, C16, dW);
+                       slab, n_parts, (int)C, (int)K, C16, dW);
     SGC_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(xent_reduce_small_kernel, dim3((unsigned)C + 1), dim3(256), 0, s, loss_part, db_part,
                        waves, (int)C, C16, 1.0 / (double)M, loss, db);
