@@ -29,6 +29,9 @@ Output: "replicated" (every rank gets all of X_K) or "sharded" (every rank
 keeps its rows of X_K, which is what ShardedSGCTrainer -- the data-parallel
 SGC classifier -- consumes; no full X_K is ever materialised).
 """
+import contextlib
+import os
+import time
 from dataclasses import dataclass
 from typing import Callable, Optional
 
@@ -1464,6 +1467,28 @@ def ctypes_void(v):
     return ctypes.c_void_p(int(v))
 
 
+# Host seconds of the set-up stages of the first partitioned call, by stage
+# (measurement: with SGC_AMD_SETUP_TRACE=1 each stage also synchronises the
+# device first, so the GPU work it queued is charged to it).
+SETUP_SECONDS = {}
+
+
+@contextlib.contextmanager
+def setup_stage(name, device=None):
+    if os.environ.get("SGC_AMD_SETUP_TRACE") != "1":
+        yield
+        return
+    if device is not None and device.type == "cuda":
+        torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    try:
+        yield
+    finally:
+        if device is not None and device.type == "cuda":
+            torch.cuda.synchronize(device)
+        SETUP_SECONDS[name] = SETUP_SECONDS.get(name, 0.0) + time.perf_counter() - t0
+
+
 def _ipc_for(prop, group, rank, world, n, ld, device):
     """The propagator's IpcPeers window for [n, ld] halves, made once
     (collective: every rank builds it in the same call); None when a rank
@@ -1473,16 +1498,20 @@ def _ipc_for(prop, group, rank, world, n, ld, device):
         return prop._ipc
     ok, ipc, why = 1, None, ""
     try:
-        ipc = IpcPeers(group, rank, world, n, ld, device)
-        if not ipc.self_test():
+        with setup_stage("ipc_window_and_handles", device):
+            ipc = IpcPeers(group, rank, world, n, ld, device)
+        with setup_stage("ipc_self_test", device):
+            passed = ipc.self_test()
+        if not passed:
             ok, why = 0, "the set-up self-test read a wrong value or timed out"
     except Exception as e:  # noqa: BLE001 -- recorded, agreed on below
         ok, why = 0, f"{type(e).__name__}: {e}"
     if world > 1:
-        dev = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
-        t = torch.tensor([ok], dtype=torch.int32, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
-        ok = int(t.item())
+        with setup_stage("ipc_agree", device):
+            dev = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+            t = torch.tensor([ok], dtype=torch.int32, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+            ok = int(t.item())
     if not ok:
         if ipc is not None:
             ipc.close()

@@ -210,14 +210,22 @@ def _host_csr(csr):
 def _propagator(csr, group, partition, staging):
     """The partitioned propagator for (adjacency, group, partition), built once
     and cached on the adjacency's CSR with its buffers and prepared launches."""
-    from .distributed import (CyclicRowPropagator, FeaturePartitionedPropagator,
-                              LinePartitionedPropagator, RowPartitionedPropagator,
-                              make_shard_device)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     key = ("dist", id(group), rank, world, partition, staging)
     prop = csr._plans.get(key)
     if prop is not None:
         return prop
+    from .distributed import setup_stage
+    with setup_stage(f"build_{partition}", csr.device):
+        prop = _build_propagator(csr, group, partition, staging, rank, world)
+    csr._plans[key] = prop
+    return prop
+
+
+def _build_propagator(csr, group, partition, staging, rank, world):
+    from .distributed import (CyclicRowPropagator, FeaturePartitionedPropagator,
+                              LinePartitionedPropagator, RowPartitionedPropagator,
+                              make_shard_device)
     if partition == "replicate":
         prop = ReplicatedPropagator(csr)
     elif partition == "features":
@@ -234,7 +242,6 @@ def _propagator(csr, group, partition, staging):
         groups = 1 if world <= 2 else 2 if world <= 4 else 3
         prop = CyclicRowPropagator(rp, ci, va, rank, world, csr.device, group=group,
                                    groups=groups, host_staging=staging)
-    csr._plans[key] = prop
     return prop
 
 
@@ -289,7 +296,9 @@ PROPAGATIONS = [0]
 
 def _run(prop, X, K):
     PROPAGATIONS[0] += 1
-    return prop.propagate(X, K, output="replicated")
+    from .distributed import setup_stage
+    with setup_stage(f"propagate_{PROPAGATIONS[0]}", X.device):
+        return prop.propagate(X, K, output="replicated")
 
 
 def _drop_propagator(csr, group, name, staging):

@@ -842,7 +842,14 @@ def warmup(device=None, units=WARM_PROPAGATE | WARM_CLASSIFIER):
             i = torch.arange(n, device=dev)
             idx = torch.stack([torch.cat([(i + 1) % n, i]), torch.cat([i, i])])
             adj = torch.sparse_coo_tensor(idx, torch.full((2 * n,), 0.5, device=dev), (n, n))
-            propagate(csr_of(adj), torch.ones((n, 8), device=dev), 2)
+            csr = csr_of(adj)
+            propagate(csr, torch.ones((n, 8), device=dev), 2)
+            # the multi-GPU partitions' device-built shards (searchsorted,
+            # indexing, casts): their torch kernels' first use cost the first
+            # P = 4 call ~0.2 s of its 0.42 (profiles/r06/s20)
+            from .distributed import _chunk_order, make_shard_device
+            make_shard_device(csr, 1, 3)
+            _chunk_order(csr, [(0, 32), (32, n)])
         torch.cuda.synchronize(dev)
         if units & WARM_PROPAGATE:
             # torch's stream pool for this device (the multi-GPU partitions'

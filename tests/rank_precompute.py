@@ -47,6 +47,9 @@ def main():
            "device": str(features.device),
            "world": dist.get_world_size() if dist.is_initialized() else 1,
            "backend": dist.get_backend() if dist.is_initialized() else None}
+    from sgc_amd.distributed import SETUP_SECONDS
+    if SETUP_SECONDS:  # SGC_AMD_SETUP_TRACE=1: the set-up stages, host seconds
+        rec["setup_seconds"] = {k: round(v, 6) for k, v in SETUP_SECONDS.items()}
     if dist.is_initialized():
         rec["auto"] = multigpu.auto_choice(csr, dist.group.WORLD, features.shape[1], 2)
         props_ = [p for p in csr._plans.values() if hasattr(p, "ipc_unavailable")]
