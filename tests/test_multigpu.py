@@ -43,8 +43,10 @@ def _torchrun_like_worker(rank, world, port, case, K, partition, q, env=None, ca
             props.append(multigpu.PROPAGATIONS[0] - before)
             outs.append(out)
         rec = multigpu.auto_choice(adj._sgc_amd_csr[1], dist.group.WORLD, X.shape[1], K)
+        from sgc_amd.distributed import SETUP_SECONDS
         q.put((rank, outs[0].numpy().copy(), all(torch.equal(outs[0], o) for o in outs),
-               dist.get_world_size(), secs >= 0, None if rec is None else dict(rec), props))
+               dist.get_world_size(), secs >= 0, None if rec is None else dict(rec), props,
+               dict(SETUP_SECONDS)))
     finally:
         import torch.distributed as dist2
         if dist2.is_initialized():
@@ -110,6 +112,23 @@ def test_auto_first_call_runs_one_partition(tiny_cases, world, name, chosen):
         rec, props = got[r][4], got[r][5]
         assert props == [1, 1, 1], props
         assert rec["chosen"] == chosen and rec["how"] == "rule", rec
+
+
+@pytest.mark.parametrize("trace", [False, True])
+def test_setup_stage_trace(tiny_cases, trace):
+    """SGC_AMD_SETUP_TRACE=1 records the first partitioned call's set-up
+    stages (the propagator's build, each propagation) by name, for the
+    first-call measurements (tests/rank_precompute.py); unset, nothing is
+    recorded and the results are the same bits."""
+    env = {"SGC_AMD_SETUP_TRACE": "1"} if trace else None
+    got = _run_world(tiny_cases["hub1000_F130"], 3, 2, "lines", env=env, calls=2)
+    for r in range(3):
+        setup = got[r][6]
+        if trace:
+            assert {"build_lines", "propagate_1", "propagate_2"} <= set(setup), setup
+            assert all(v >= 0 for v in setup.values())
+        else:
+            assert setup == {}
 
 
 def test_tune_times_on_the_second_call_and_persists(tiny_cases, tmp_path):
